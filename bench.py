@@ -1,0 +1,233 @@
+#!/usr/bin/env python3
+"""bench.py -- MI355X Snappy codec benchmark (BASELINE.json metric).
+
+One step = one compress (K1 block compress + K3 scan/gather) and one
+decompress (K4) of the per-GPU batch, inputs already resident in HBM.
+Default workload = BASELINE.json configs[1]: 1 GiB of synthetic enwik8-like
+text as 32,768 independent 32 KiB streams (each == the reference's
+snappy_compress() of its chunk), per GPU (weak scaling: every rank gets its
+own 1 GiB shard of the generator; the only exchange is the 8-byte size
+all-gather that places each shard in the global stream).  --assemble adds
+the RCCL all-gather of the compressed shards (timed separately).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload text32k|text64k|random|repeat]
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "lightweight-snappy_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import datagen  # noqa: E402
+import snappy_amd  # noqa: E402
+
+METRIC = "compress + decompress MB/s at 1/2/4/8 MI355X; % HBM roofline; ratio vs ref"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+WORKLOADS = {
+    # name: (generator kind, seed, layout, chunk, description)
+    "text32k": ("T", 1234, snappy_amd.STREAMS, 32768,
+                "1 GiB/GPU synthetic enwik8-like text as 32,768 independent 32 KiB snappy_compress() streams"),
+    "text64k": ("T", 1234, snappy_amd.SINGLE, 65536,
+                "1 GiB/GPU synthetic text as one snappy_compress() stream of 65,536-byte blocks"),
+    "random": ("R", 1, snappy_amd.SINGLE, 65536, "1 GiB/GPU random bytes (all-literal), one stream"),
+    "repeat": ("P", 2, snappy_amd.SINGLE, 65536, "1 GiB/GPU 64-byte-period repeat (all-copy), one stream"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="text32k", choices=sorted(WORKLOADS))
+    ap.add_argument("--bytes-per-gpu", type=int, default=1 << 30)
+    ap.add_argument("--assemble", action="store_true", help="also time the RCCL all-gather of shards")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-bytes", type=int, default=1 << 30)
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
+                    help="rocprofv3 PMC summary giving HBM traffic per launch (see profiles/README.md)")
+    return ap.parse_args()
+
+
+def cpu_baseline(kind: str, seed: int, chunk: int, layout: int, sample: int) -> dict:
+    """The oracle (CPU restatement, fixture-verified bit-exact with the
+    reference) timed on this host, 1 thread like the reference, wall clock."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the CPU baseline leg only
+
+    a = datagen.make(kind, sample, seed)
+    t0 = time.perf_counter()
+    if layout == snappy_amd.STREAMS:
+        payload, offs = oracle.compress_streams(a, chunk, threads=1)
+    else:
+        payload = np.frombuffer(oracle.compress(a), dtype=np.uint8)
+    t1 = time.perf_counter()
+    if layout == snappy_amd.STREAMS:
+        back = oracle.decompress_streams(payload, offs, a.size, chunk, threads=1)
+    else:
+        back = np.frombuffer(oracle.decompress(payload.tobytes()), dtype=np.uint8)
+    t2 = time.perf_counter()
+    assert np.array_equal(back, a)
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(a.size / (t2 - t0) / 1e6, 2), "unit": "MB/s", "cores": 1, "kind": "port",
+            "sample": f"{a.size / 2**20:.0f} MiB of the same workload, compress {a.size / (t1 - t0) / 1e6:.1f} MB/s"
+                      f" + decompress {a.size / (t2 - t1) / 1e6:.1f} MB/s, oracle/snappy_oracle.c -O2, 1 thread,"
+                      f" {cpu_model}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    kind, seed, layout, chunk, desc = WORKLOADS[args.workload]
+    n = args.bytes_per_gpu
+    host = np.empty(n, dtype=np.uint8)
+    datagen.fill(host, kind, seed, offset=rank * n, threads=16)
+    x = torch.from_numpy(host).to(dev)
+    codec = snappy_amd.Codec(dev.index)
+    codec.enable_timing(True)
+    stream = torch.cuda.current_stream(dev)
+    codec.set_stream(stream.cuda_stream)
+    units = codec.num_units(n, chunk, layout)
+    out = torch.empty(codec.max_output(n, chunk, layout), dtype=torch.uint8, device=dev)
+    offs = torch.empty(units + 1, dtype=torch.int64, device=dev)
+    back = torch.empty(n, dtype=torch.uint8, device=dev)
+    # SINGLE layout sharded over ranks: rank 0 carries the global preamble
+    flags = snappy_amd.NO_PREAMBLE if (layout == snappy_amd.SINGLE and rank > 0) else 0
+    header_value = n * world if layout == snappy_amd.SINGLE else n
+    sizes_t = torch.zeros(world, dtype=torch.int64, device=dev)
+
+    def step():
+        clen = codec.compress_ptr_ex(x.data_ptr(), n, chunk, layout, flags, header_value, out.data_ptr(),
+                                     offs.data_ptr())
+        if world > 1:  # C1: shard sizes -> global stream offsets
+            mine = torch.tensor([clen], dtype=torch.int64, device=dev)
+            dist.all_gather_into_tensor(sizes_t, mine)
+        codec.decompress_ptr_ex(out.data_ptr(), offs.data_ptr(), n, chunk, layout, flags, header_value,
+                                back.data_ptr(), check=False)
+        return clen
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    k1, k3, k4 = [], [], []
+    t0 = time.perf_counter()
+    clen = 0
+    for _ in range(args.steps):
+        clen = step()
+        a, b, c = codec.last_timings()
+        k1.append(a), k3.append(b), k4.append(c)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    st = codec.decompress_status()
+    ok = st == 0 and bool(torch.equal(back, x))
+    if world > 1:
+        t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, bad = float(t[0]), float(t[1])
+        ok = bad == 0.0
+        tot = torch.tensor([clen], dtype=torch.int64, device=dev)
+        dist.all_reduce(tot)
+        total_comp = int(tot)
+    else:
+        total_comp = clen
+
+    assemble = None
+    if args.assemble and world > 1:  # C2: every rank receives the whole stream
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        ta = time.perf_counter()
+        mx = int(sizes_t.max())
+        pad = torch.zeros(mx, dtype=torch.uint8, device=dev)
+        pad[:clen] = out[:clen]
+        full = torch.empty(world * mx, dtype=torch.uint8, device=dev)
+        dist.all_gather_into_tensor(full, pad)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        tb = time.perf_counter() - ta
+        assemble = {"allgather_ms": round(tb * 1e3, 3), "bytes": int(world * mx),
+                    "GBps_per_rank_in": round((world - 1) * mx / tb / 1e9, 2)}
+
+    total_in = n * world
+    ms_step = elapsed / args.steps * 1e3
+    value = total_in / (elapsed / args.steps) / 1e6
+    k1m, k3m, k4m = (float(np.mean(v)) for v in (k1, k3, k4))
+    comp_bytes = clen  # this rank's compressed output (rank 0)
+    achieved = (n + comp_bytes) / (k1m * 1e-3) / 1e9
+    traffic = None
+    try:
+        pm = json.load(open(args.pmc))
+        if pm.get("workload") == args.workload and pm.get("bytes_per_gpu") == n:
+            traffic = pm.get("k1_hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(kind, seed, chunk, layout, min(args.cpu_sample_bytes, n))
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": f"{args.workload}: {desc}; one step = compress + decompress round trip",
+                       "bytes_per_gpu": n, "chunk": chunk, "layout": "STREAMS" if layout else "SINGLE",
+                       "units_per_gpu": units, "parallelism": f"dp{world} (block shards)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "kernel": "k1_compress_units", "algorithmic_bytes_per_launch": n + comp_bytes},
+            "cpu_baseline": cpu,
+            "ratio": round(total_in / total_comp, 4),
+            "compress_MBps": round(n / ((k1m + k3m) * 1e-3) / 1e6, 1),
+            "decompress_MBps": round(n / (k4m * 1e-3) / 1e6, 1),
+            "kernel_ms": {"k1_compress": round(k1m, 3), "k3_scan_gather": round(k3m, 3),
+                          "k4_decompress": round(k4m, 3)},
+            "k4_roofline_frac": round((n + comp_bytes) / (k4m * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+            "round_trip_ok": ok,
+        }
+        if assemble:
+            line["assemble"] = assemble
+        print(json.dumps(line), flush=True)
+    codec.close()
+    if world > 1:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

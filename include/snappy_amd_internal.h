@@ -1,0 +1,23 @@
+/*
+ * snappy_amd_internal.h -- host-buffer entry points of the HIP shim
+ * (snappy_device.hip) that the C host layer (snappy_host.c) builds the
+ * reference FILE* API on.  Exported for the host layer; not part of the
+ * documented drop-in surface.
+ */
+#ifndef SNAPPY_AMD_INTERNAL_H
+#define SNAPPY_AMD_INTERNAL_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* One SINGLE-layout stream of in[0..n) whose preamble encodes
+ * header_value (snappy_compress writes its input_size argument, which the
+ * reference never checks against the bytes read: snappy_compression.c:171). */
+int snappy_amd_host_compress(const uint8_t *in, size_t n, uint64_t header_value, uint8_t *out, size_t cap,
+                             size_t *out_len);
+int snappy_amd_host_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len);
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,8 @@
+/* Drop-in replacement of src/snappy_compression_tree.h:10 (tturturiello/lightweight-snappy).
+ * The BST matcher (-b) is outside the GPU hot path:
+ * libsnappy_amd.so exports the symbol and reports SNAPPY_AMD_ERR_UNSUPPORTED. */
+#ifndef SNAPPY_SNAPPY_COMPRESSION_TREE_H
+#define SNAPPY_SNAPPY_COMPRESSION_TREE_H
+#include <stdio.h>
+int snappy_compress_bst(FILE *file_input, unsigned long long input_size, FILE *file_compressed);
+#endif

@@ -1,0 +1,87 @@
+/*
+ * cmd.c -- `snappy [-c|-b|-d] [-r] infile outfile`, the CLI of the reference
+ * (src/cmd.c:19-105: same flags, same last-two-argv file names, usage +
+ * exit(1) on argc < 4), linked against the MI355X library instead of the CPU
+ * codec.  -r prints sizes, ratio and MB/s (MB = 1e6 B, wall clock).
+ */
+#include <errno.h>
+#include <getopt.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "snappy_amd.h"
+
+static void usage(void)
+{
+    fprintf(stderr,
+            "snappy [-c|-d|-b] [-r] [infile] [outfile]\n"
+            "-c compress (MI355X)\n"
+            "-b compress with the BST matcher (not supported on MI355X)\n"
+            "-d decompress (MI355X)\n"
+            "-r print results\n");
+    exit(EXIT_FAILURE);
+}
+
+static FILE *open_or_die(const char *name, const char *mode)
+{
+    FILE *f = fopen(name, mode);
+    if (!f) {
+        fprintf(stderr, "cannot open %s: %s\n", name, strerror(errno));
+        exit(EXIT_FAILURE);
+    }
+    return f;
+}
+
+static unsigned long long file_size(FILE *f)
+{
+    fseek(f, 0, SEEK_END);
+    long s = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    return s < 0 ? 0 : (unsigned long long)s;
+}
+
+int main(int argc, char *argv[])
+{
+    enum { M_COMPRESS, M_BST, M_DECOMPRESS } mode = M_COMPRESS;
+    int show = 0, opt;
+    if (argc < 4) usage();
+    while ((opt = getopt(argc, argv, "cbdr")) != -1) {
+        if (opt == 'c') mode = M_COMPRESS;
+        else if (opt == 'b') mode = M_BST;
+        else if (opt == 'd') mode = M_DECOMPRESS;
+        else if (opt == 'r') show = 1;
+        else usage();
+    }
+    const char *in_name = argv[argc - 2], *out_name = argv[argc - 1];
+    FILE *in = open_or_die(in_name, "rb");
+    FILE *out = open_or_die(out_name, "wb");
+    unsigned long long in_size = file_size(in);
+
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    int rc = 0;
+    if (mode == M_COMPRESS) {
+        snappy_compress(in, in_size, out);
+        rc = snappy_amd_last_status();
+    } else if (mode == M_BST) {
+        rc = snappy_compress_bst(in, in_size, out);
+    } else {
+        rc = snappy_decompress(in, out);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    fclose(in);
+    fclose(out);
+    double secs = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+    if (show) {
+        FILE *o = open_or_die(out_name, "rb");
+        unsigned long long out_size = file_size(o);
+        fclose(o);
+        unsigned long long raw = mode == M_DECOMPRESS ? out_size : in_size;
+        printf("input %llu bytes, output %llu bytes\n", in_size, out_size);
+        if (mode != M_DECOMPRESS && out_size) printf("ratio %f\n", (double)in_size / (double)out_size);
+        printf("%f s, %f MB/s (uncompressed bytes)\n", secs, secs > 0 ? raw / (secs * 1e6) : 0.0);
+    }
+    return rc == 0 ? 0 : 1;
+}

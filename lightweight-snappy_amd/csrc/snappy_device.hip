@@ -1,0 +1,377 @@
+// snappy_device.hip -- the thin extern "C" shim between the C host code and
+// the gfx950 kernels: device memory, the launch stream, HIP events and the
+// launch geometry.  Declared in include/snappy_amd.h (device batch API) and
+// include/snappy_amd_internal.h (host-buffer helpers used by snappy_host.c).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <mutex>
+
+#include "snappy_amd.h"
+#include "snappy_amd_internal.h"
+#include "snappy_kernels.h"
+
+using namespace snappy_amd;
+
+struct snappy_amd_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    uint8_t *scratch = nullptr;
+    size_t scratch_cap = 0;
+    uint32_t *sizes = nullptr;
+    size_t sizes_cap = 0;
+    int32_t *status = nullptr;
+    size_t status_cap = 0;
+    uint64_t *total = nullptr;      // device u64
+    int64_t *k5res = nullptr;       // device i64[3]
+    uint64_t *h_total = nullptr;    // pinned
+    int32_t *h_status = nullptr;    // pinned, grows with status_cap
+    size_t h_status_cap = 0;
+    size_t last_units = 0;
+    // host-buffer path staging
+    uint8_t *d_a = nullptr; size_t d_a_cap = 0;
+    uint8_t *d_b = nullptr; size_t d_b_cap = 0;
+    uint64_t *d_idx = nullptr; size_t d_idx_cap = 0;
+    bool timing = false;
+    hipEvent_t ev[5] = {};
+    float k1_ms = 0, k3_ms = 0, k4_ms = 0;
+};
+
+#define HIP_OK(expr) do { if ((expr) != hipSuccess) return SNAPPY_AMD_ERR_DEVICE; } while (0)
+
+static int grow(void **ptr, size_t *cap, size_t need)
+{
+    if (need <= *cap) return SNAPPY_AMD_OK;
+    if (*ptr) (void)hipFree(*ptr);
+    *ptr = nullptr;
+    *cap = 0;
+    size_t want = need + need / 8 + 4096;
+    if (hipMalloc(ptr, want) != hipSuccess) { *ptr = nullptr; return SNAPPY_AMD_ERR_DEVICE; }
+    *cap = want;
+    return SNAPPY_AMD_OK;
+}
+
+static size_t k1_lds_bytes(uint32_t unit) { return 8192 + ((unit + 15) & ~15u) + 32; }
+static size_t k4_lds_bytes(uint32_t unit, uint32_t comp_cap) { return ((unit + 15) & ~15u) + 16 + comp_cap + 32; }
+
+extern "C" {
+
+int snappy_amd_create(int device, snappy_amd_ctx **out)
+{
+    if (!out) return SNAPPY_AMD_ERR_ARG;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0 || device < 0 || device >= count)
+        return SNAPPY_AMD_ERR_DEVICE;
+    HIP_OK(hipSetDevice(device));
+    snappy_amd_ctx *c = new snappy_amd_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return SNAPPY_AMD_ERR_DEVICE; }
+    c->stream = c->own;
+    if (hipMalloc(&c->total, 64) != hipSuccess || hipMalloc(&c->k5res, 64) != hipSuccess ||
+        hipHostMalloc(&c->h_total, 64, hipHostMallocDefault) != hipSuccess) {
+        snappy_amd_destroy(c);
+        return SNAPPY_AMD_ERR_DEVICE;
+    }
+    for (int i = 0; i < 5; i++) (void)hipEventCreate(&c->ev[i]);
+    // K1/K4 use up to 72 KiB / 132 KiB of dynamic LDS with 65,536-byte units
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k1_compress_units),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k4_decompress_units),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    *out = c;
+    return SNAPPY_AMD_OK;
+}
+
+void snappy_amd_destroy(snappy_amd_ctx *c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    void *bufs[] = {c->scratch, c->sizes, c->status, c->total, c->k5res, c->d_a, c->d_b, c->d_idx};
+    for (void *b : bufs) if (b) (void)hipFree(b);
+    if (c->h_total) (void)hipHostFree(c->h_total);
+    if (c->h_status) (void)hipHostFree(c->h_status);
+    for (int i = 0; i < 5; i++) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+}
+
+int snappy_amd_set_stream(snappy_amd_ctx *c, void *s)
+{
+    if (!c) return SNAPPY_AMD_ERR_ARG;
+    c->stream = s ? static_cast<hipStream_t>(s) : c->own;
+    return SNAPPY_AMD_OK;
+}
+
+void *snappy_amd_get_stream(snappy_amd_ctx *c) { return c ? c->stream : nullptr; }
+
+int snappy_amd_enable_timing(snappy_amd_ctx *c, int on)
+{
+    if (!c) return SNAPPY_AMD_ERR_ARG;
+    c->timing = on != 0;
+    return SNAPPY_AMD_OK;
+}
+
+int snappy_amd_last_timings(snappy_amd_ctx *c, float *k1, float *k3, float *k4)
+{
+    if (!c) return SNAPPY_AMD_ERR_ARG;
+    if (c->timing) {
+        // resolve whatever the stream has recorded so far (waits for it)
+        (void)hipSetDevice(c->device);
+        if (hipEventSynchronize(c->ev[2]) == hipSuccess) {
+            (void)hipEventElapsedTime(&c->k1_ms, c->ev[0], c->ev[1]);
+            (void)hipEventElapsedTime(&c->k3_ms, c->ev[1], c->ev[2]);
+        }
+        if (c->last_units && hipEventSynchronize(c->ev[4]) == hipSuccess)
+            (void)hipEventElapsedTime(&c->k4_ms, c->ev[3], c->ev[4]);
+    }
+    if (k1) *k1 = c->k1_ms;
+    if (k3) *k3 = c->k3_ms;
+    if (k4) *k4 = c->k4_ms;
+    return SNAPPY_AMD_OK;
+}
+
+size_t snappy_amd_num_units(size_t n, uint32_t chunk, int layout)
+{
+    uint32_t unit = layout == SNAPPY_AMD_SINGLE ? SNAPPY_AMD_BLOCK : chunk;
+    if (unit == 0) return 0;
+    return (n + unit - 1) / unit;
+}
+
+size_t snappy_amd_max_output(size_t n, uint32_t chunk, int layout)
+{
+    uint32_t unit = layout == SNAPPY_AMD_SINGLE ? SNAPPY_AMD_BLOCK : chunk;
+    if (unit == 0) return 0;
+    size_t units = (n + unit - 1) / unit;
+    return n + units * (unit / 32 + 32) + 16;
+}
+
+static uint32_t hdr_mode_of(int layout, uint32_t flags)
+{
+    if (layout == SNAPPY_AMD_STREAMS) return SNAPPY_HDR_EVERY_UNIT;
+    return (flags & SNAPPY_AMD_NO_PREAMBLE) ? SNAPPY_HDR_NONE : SNAPPY_HDR_FIRST_UNIT;
+}
+
+static int compress_impl(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t chunk, int layout, uint32_t flags,
+                         uint64_t header_value, void *d_out, uint64_t *d_offsets, size_t *out_len)
+{
+    if (!c || (!d_in && n) || !d_out || !d_offsets) return SNAPPY_AMD_ERR_ARG;
+    if (layout != SNAPPY_AMD_SINGLE && layout != SNAPPY_AMD_STREAMS) return SNAPPY_AMD_ERR_ARG;
+    const uint32_t unit = layout == SNAPPY_AMD_SINGLE ? SNAPPY_AMD_BLOCK : chunk;
+    if (unit == 0 || unit > SNAPPY_AMD_BLOCK) return SNAPPY_AMD_ERR_ARG;
+    HIP_OK(hipSetDevice(c->device));
+    if (n == 0) {
+        // src/snappy_compression.c:417-421: no block, so no header either
+        HIP_OK(hipMemsetAsync(d_offsets, 0, sizeof(uint64_t), c->stream));
+        if (out_len) *out_len = 0;
+        return SNAPPY_AMD_OK;
+    }
+    const size_t units = (n + unit - 1) / unit;
+    const uint64_t stride = unit_stride(unit);
+    int rc;
+    if ((rc = grow(reinterpret_cast<void **>(&c->scratch), &c->scratch_cap, units * stride))) return rc;
+    if ((rc = grow(reinterpret_cast<void **>(&c->sizes), &c->sizes_cap, units * sizeof(uint32_t)))) return rc;
+    const uint32_t vec_ok = ((reinterpret_cast<uintptr_t>(d_in) | unit) & 15) == 0;
+    if (c->timing) (void)hipEventRecord(c->ev[0], c->stream);
+    hipLaunchKernelGGL(k1_compress_units, dim3((uint32_t)units), dim3(64), k1_lds_bytes(unit), c->stream,
+                       static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hdr_mode_of(layout, flags), header_value,
+                       vec_ok,
+                       c->scratch, stride, c->sizes);
+    HIP_OK(hipGetLastError());
+    if (c->timing) (void)hipEventRecord(c->ev[1], c->stream);
+    hipLaunchKernelGGL(k3_scan, dim3(1), dim3(1024), 0, c->stream, c->sizes, (uint64_t)units, d_offsets, c->total);
+    hipLaunchKernelGGL(k3_gather, dim3((uint32_t)units), dim3(256), 0, c->stream, c->scratch, stride, c->sizes,
+                       d_offsets, static_cast<uint8_t *>(d_out));
+    HIP_OK(hipGetLastError());
+    if (c->timing) (void)hipEventRecord(c->ev[2], c->stream);
+    if (out_len) {
+        HIP_OK(hipMemcpyAsync(c->h_total, c->total, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipStreamSynchronize(c->stream));
+        *out_len = (size_t)*c->h_total;
+        if (c->timing) {
+            (void)hipEventElapsedTime(&c->k1_ms, c->ev[0], c->ev[1]);
+            (void)hipEventElapsedTime(&c->k3_ms, c->ev[1], c->ev[2]);
+        }
+    }
+    return SNAPPY_AMD_OK;
+}
+
+int snappy_amd_compress_device(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t chunk, int layout, void *d_out,
+                               uint64_t *d_offsets, size_t *out_len)
+{
+    return compress_impl(c, d_in, n, chunk, layout, 0, (uint64_t)n, d_out, d_offsets, out_len);
+}
+
+int snappy_amd_compress_device_ex(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t chunk, int layout,
+                                  uint32_t flags, uint64_t header_value, void *d_out, uint64_t *d_offsets,
+                                  size_t *out_len)
+{
+    return compress_impl(c, d_in, n, chunk, layout, flags, header_value, d_out, d_offsets, out_len);
+}
+
+static int decompress_launch(snappy_amd_ctx *c, const void *d_comp, const uint64_t *d_offsets, size_t n,
+                             uint32_t chunk, int layout, uint32_t flags, uint64_t header_value, void *d_out)
+{
+    if (!c || !d_comp || !d_offsets || (!d_out && n)) return SNAPPY_AMD_ERR_ARG;
+    if (layout != SNAPPY_AMD_SINGLE && layout != SNAPPY_AMD_STREAMS) return SNAPPY_AMD_ERR_ARG;
+    const uint32_t unit = layout == SNAPPY_AMD_SINGLE ? SNAPPY_AMD_BLOCK : chunk;
+    if (unit == 0 || unit > SNAPPY_AMD_BLOCK) return SNAPPY_AMD_ERR_ARG;
+    if (reinterpret_cast<uintptr_t>(d_comp) & 3) return SNAPPY_AMD_ERR_ARG;
+    HIP_OK(hipSetDevice(c->device));
+    c->last_units = 0;
+    if (n == 0) return SNAPPY_AMD_OK;
+    const size_t units = (n + unit - 1) / unit;
+    int rc;
+    if ((rc = grow(reinterpret_cast<void **>(&c->status), &c->status_cap, units * sizeof(int32_t)))) return rc;
+    // a unit's compressed size is bounded by the encoder's worst case; the
+    // decoder rejects (TRUNCATED) anything larger than this LDS window.
+    const uint32_t comp_cap = (uint32_t)(((uint64_t)unit + unit / 32 + 64 + 15) & ~15ull);
+    if (c->timing) (void)hipEventRecord(c->ev[3], c->stream);
+    hipLaunchKernelGGL(k4_decompress_units, dim3((uint32_t)units), dim3(64), k4_lds_bytes(unit, comp_cap), c->stream,
+                       static_cast<const uint8_t *>(d_comp), d_offsets, (uint64_t)n, unit, hdr_mode_of(layout, flags),
+                       header_value, comp_cap,
+                       static_cast<uint8_t *>(d_out), c->status);
+    HIP_OK(hipGetLastError());
+    if (c->timing) (void)hipEventRecord(c->ev[4], c->stream);
+    c->last_units = units;
+    return SNAPPY_AMD_OK;
+}
+
+int snappy_amd_decompress_status(snappy_amd_ctx *c)
+{
+    if (!c) return SNAPPY_AMD_ERR_ARG;
+    if (c->last_units == 0) return SNAPPY_AMD_OK;
+    HIP_OK(hipSetDevice(c->device));
+    const size_t bytes = c->last_units * sizeof(int32_t);
+    if (bytes > c->h_status_cap) {
+        if (c->h_status) (void)hipHostFree(c->h_status);
+        c->h_status = nullptr;
+        c->h_status_cap = 0;
+        HIP_OK(hipHostMalloc(&c->h_status, bytes, hipHostMallocDefault));
+        c->h_status_cap = bytes;
+    }
+    HIP_OK(hipMemcpyAsync(c->h_status, c->status, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    if (c->timing) (void)hipEventElapsedTime(&c->k4_ms, c->ev[3], c->ev[4]);
+    for (size_t i = 0; i < c->last_units; i++)
+        if (c->h_status[i] != SNAPPY_ST_OK) return c->h_status[i];
+    return SNAPPY_AMD_OK;
+}
+
+int snappy_amd_decompress_device_async(snappy_amd_ctx *c, const void *d_comp, const uint64_t *d_offsets, size_t n,
+                                       uint32_t chunk, int layout, void *d_out)
+{
+    return decompress_launch(c, d_comp, d_offsets, n, chunk, layout, 0, (uint64_t)n, d_out);
+}
+
+int snappy_amd_decompress_device_ex(snappy_amd_ctx *c, const void *d_comp, const uint64_t *d_offsets, size_t n,
+                                    uint32_t chunk, int layout, uint32_t flags, uint64_t header_value, void *d_out,
+                                    int sync)
+{
+    int rc = decompress_launch(c, d_comp, d_offsets, n, chunk, layout, flags, header_value, d_out);
+    if (rc || !sync) return rc;
+    return snappy_amd_decompress_status(c);
+}
+
+int snappy_amd_decompress_device(snappy_amd_ctx *c, const void *d_comp, const uint64_t *d_offsets, size_t n,
+                                 uint32_t chunk, int layout, void *d_out)
+{
+    int rc = decompress_launch(c, d_comp, d_offsets, n, chunk, layout, 0, (uint64_t)n, d_out);
+    if (rc) return rc;
+    return snappy_amd_decompress_status(c);
+}
+
+int snappy_amd_index_device(snappy_amd_ctx *c, const void *d_comp, size_t clen, uint64_t *d_offsets, size_t max_units,
+                            size_t *n_out)
+{
+    if (!c || !d_comp || !d_offsets) return SNAPPY_AMD_ERR_ARG;
+    HIP_OK(hipSetDevice(c->device));
+    hipLaunchKernelGGL(k5_index_stream, dim3(1), dim3(64), 0, c->stream, static_cast<const uint8_t *>(d_comp),
+                       (uint64_t)clen, d_offsets, (uint64_t)max_units, c->k5res);
+    HIP_OK(hipGetLastError());
+    int64_t res[3];
+    HIP_OK(hipMemcpyAsync(res, c->k5res, sizeof(res), hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    if (n_out) *n_out = (size_t)res[1];
+    return (int)res[0];
+}
+
+// ---- host-buffer helpers (used by snappy_host.c) -------------------------
+
+static std::mutex g_mu;
+static snappy_amd_ctx *g_ctx = nullptr;
+
+static int global_ctx(snappy_amd_ctx **out)
+{
+    if (!g_ctx) {
+        int dev = 0;
+        const char *e = getenv("SNAPPY_AMD_DEVICE");
+        if (e) dev = atoi(e);
+        int rc = snappy_amd_create(dev, &g_ctx);
+        if (rc) { g_ctx = nullptr; return rc; }
+    }
+    *out = g_ctx;
+    return SNAPPY_AMD_OK;
+}
+
+int snappy_amd_host_compress(const uint8_t *in, size_t n, uint64_t header_value, uint8_t *out, size_t cap,
+                             size_t *out_len)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!out_len || (!in && n)) return SNAPPY_AMD_ERR_ARG;
+    *out_len = 0;
+    if (n == 0) return SNAPPY_AMD_OK;
+    snappy_amd_ctx *c;
+    int rc = global_ctx(&c);
+    if (rc) return rc;
+    HIP_OK(hipSetDevice(c->device));
+    const size_t units = (n + SNAPPY_AMD_BLOCK - 1) / SNAPPY_AMD_BLOCK;
+    const size_t maxo = snappy_amd_max_output(n, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE);
+    if ((rc = grow(reinterpret_cast<void **>(&c->d_a), &c->d_a_cap, n + 16))) return rc;
+    if ((rc = grow(reinterpret_cast<void **>(&c->d_b), &c->d_b_cap, maxo))) return rc;
+    if ((rc = grow(reinterpret_cast<void **>(&c->d_idx), &c->d_idx_cap, (units + 1) * sizeof(uint64_t)))) return rc;
+    HIP_OK(hipMemcpyAsync(c->d_a, in, n, hipMemcpyHostToDevice, c->stream));
+    size_t len = 0;
+    rc = compress_impl(c, c->d_a, n, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE, 0, header_value, c->d_b, c->d_idx, &len);
+    if (rc) return rc;
+    if (len > cap) return SNAPPY_AMD_ERR_CAPACITY;
+    HIP_OK(hipMemcpyAsync(out, c->d_b, len, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    *out_len = len;
+    return SNAPPY_AMD_OK;
+}
+
+int snappy_amd_host_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!out_len || (!in && n)) return SNAPPY_AMD_ERR_ARG;
+    *out_len = 0;
+    if (n == 0) return SNAPPY_AMD_OK;
+    uint64_t N = 0;
+    if (snappy_varint_decode(in, n, &N) == 0) return SNAPPY_AMD_ERR_HEADER;
+    if (N > cap) return SNAPPY_AMD_ERR_CAPACITY;
+    snappy_amd_ctx *c;
+    int rc = global_ctx(&c);
+    if (rc) return rc;
+    HIP_OK(hipSetDevice(c->device));
+    const size_t units = (N + SNAPPY_AMD_BLOCK - 1) / SNAPPY_AMD_BLOCK;
+    if ((rc = grow(reinterpret_cast<void **>(&c->d_a), &c->d_a_cap, n + 16))) return rc;
+    if ((rc = grow(reinterpret_cast<void **>(&c->d_b), &c->d_b_cap, N + 16))) return rc;
+    if ((rc = grow(reinterpret_cast<void **>(&c->d_idx), &c->d_idx_cap, (units + 2) * sizeof(uint64_t)))) return rc;
+    HIP_OK(hipMemcpyAsync(c->d_a, in, n, hipMemcpyHostToDevice, c->stream));
+    size_t got = 0;
+    rc = snappy_amd_index_device(c, c->d_a, n, c->d_idx, units + 1, &got);
+    if (rc) return rc;
+    if (N == 0) { *out_len = 0; return SNAPPY_AMD_OK; }
+    rc = snappy_amd_decompress_device(c, c->d_a, c->d_idx, (size_t)N, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE, c->d_b);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(out, c->d_b, N, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    *out_len = (size_t)N;
+    return SNAPPY_AMD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,48 @@
+// snappy_kernels.h -- private declarations shared by the HIP kernels and
+// the extern "C" device shim.  Not part of the public C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SNAPPY_LAYOUT_SINGLE 0
+#define SNAPPY_LAYOUT_STREAMS 1
+#define SNAPPY_BLOCK 65536u
+
+// which units carry a varint preamble
+#define SNAPPY_HDR_NONE 0        // a SINGLE-layout shard continuing a stream
+#define SNAPPY_HDR_FIRST_UNIT 1  // unit 0 = start of a SINGLE stream
+#define SNAPPY_HDR_EVERY_UNIT 2  // STREAMS layout: every unit is a stream
+
+// per-unit status values (same numbers as SNAPPY_AMD_ERR_* in snappy_amd.h)
+#define SNAPPY_ST_OK 0
+#define SNAPPY_ST_HEADER (-2)
+#define SNAPPY_ST_TRUNCATED (-3)
+#define SNAPPY_ST_OFFSET (-4)
+#define SNAPPY_ST_OVERRUN (-5)
+#define SNAPPY_ST_CAPACITY (-6)
+#define SNAPPY_ST_UNSUPPORTED (-9)
+
+namespace snappy_amd {
+
+// bytes of fixed-stride scratch per unit: worst-case element expansion plus
+// a 10-byte preamble, padded to 16 for aligned slot starts.
+__host__ __device__ inline uint64_t unit_stride(uint32_t unit)
+{
+    return ((uint64_t)unit + unit / 32 + 16 + 16 + 15) & ~15ull;
+}
+
+__global__ void k1_compress_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit, uint32_t hdr_mode,
+                                  uint64_t header_value, uint32_t vec_ok, uint8_t *__restrict__ scratch,
+                                  uint64_t stride, uint32_t *__restrict__ sizes);
+__global__ void k3_scan(const uint32_t *__restrict__ sizes, uint64_t count, uint64_t *__restrict__ offsets,
+                        uint64_t *__restrict__ total);
+__global__ void k3_gather(const uint8_t *__restrict__ scratch, uint64_t stride, const uint32_t *__restrict__ sizes,
+                          const uint64_t *__restrict__ offsets, uint8_t *__restrict__ out);
+__global__ void k4_decompress_units(const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets,
+                                    uint64_t n, uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
+                                    uint32_t comp_cap,
+                                    uint8_t *__restrict__ out, int32_t *__restrict__ status);
+__global__ void k5_index_stream(const uint8_t *__restrict__ comp, uint64_t clen, uint64_t *__restrict__ offsets,
+                                uint64_t max_units, int64_t *__restrict__ result);
+
+}  // namespace snappy_amd

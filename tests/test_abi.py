@@ -1,0 +1,76 @@
+"""CPU: the C-ABI library loads and exports every function include/*.h
+declares; pure host helpers (varint) behave like src/varint.c.  No kernel is
+launched here."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import snappy_amd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INC = os.path.join(ROOT, "include")
+
+
+def declared_functions():
+    names = set()
+    for h in os.listdir(INC):
+        if not h.endswith(".h"):
+            continue
+        src = open(os.path.join(INC, h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w \*]*?\b(\w+)\s*\([^;{]*\)\s*;", src, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_headers_declare_the_reference_entry_points():
+    names = declared_functions()
+    for must in ("snappy_compress", "snappy_decompress", "snappy_compress_bst"):
+        assert must in names
+    assert len(names) >= 25
+
+
+def test_library_exports_every_declared_symbol():
+    lib = snappy_amd.lib()
+    missing = [n for n in sorted(declared_functions()) if not hasattr(lib, n)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", snappy_amd.LIB_PATH], capture_output=True, text=True).stdout
+    for n in declared_functions():
+        assert re.search(rf"\bT {n}$", out, flags=re.M), n
+
+
+def test_python_binding_covers_header():
+    assert declared_functions() <= set(snappy_amd._SIGS)
+
+
+def test_varint_host(golden):
+    for k in golden["varint"]:
+        assert snappy_amd.varint_encode(k["n"]).hex() == k["hex"]
+        v, used = snappy_amd.varint_decode(bytes.fromhex(k["hex"]))
+        assert (v, used) == (k["n"], len(k["hex"]) // 2)
+    # 64-bit lengths (varint.c:28-42 overflows its int at 2^31)
+    for n in (2**31, 5 * 2**30, 64 * 2**30, 2**63):
+        v, used = snappy_amd.varint_decode(snappy_amd.varint_encode(n))
+        assert v == n
+    assert snappy_amd.varint_decode(b"\x80\x80")[1] == 0
+
+
+def test_cli_usage_without_args():
+    exe = os.path.join(ROOT, "lightweight-snappy_amd", "snappy")
+    r = subprocess.run([exe], capture_output=True)
+    assert r.returncode == 1 and b"snappy [-c|-d|-b]" in r.stderr
+
+
+def test_no_oracle_in_product():
+    # the product package must never load the checker
+    pkg = os.path.join(ROOT, "lightweight-snappy_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".c", ".hip", ".h", "Makefile")):
+                src = open(os.path.join(dirpath, f), errors="ignore").read()
+                assert "liboracle" not in src and "import oracle" not in src, f
+    out = subprocess.run(["ldd", snappy_amd.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle" not in out and "snappy_ref" not in out

@@ -1,0 +1,176 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden vectors of
+the compiled reference and against the oracle on the same seeded inputs.
+Integer/byte work: the bar is bit-exact."""
+import hashlib
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import datagen
+import oracle
+import snappy_amd
+from golden_inputs import make_input
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+def to_dev(a: np.ndarray):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def test_golden_entries_host_api(golden):
+    for e in golden["entries"]:
+        data = make_input(e["spec"])
+        out = snappy_amd.compress(data)
+        assert len(out) == e["out_len"], e["name"]
+        assert sha(out) == e["out_sha256"], e["name"]
+        assert snappy_amd.decompress(out) == data, e["name"]
+
+
+def test_decoder_vectors(golden):
+    for v in golden["decoder_vectors"]:
+        assert snappy_amd.decompress(bytes.fromhex(v["stream_hex"])).hex() == v["out_hex"], v["name"]
+
+
+def test_single_layout_device(codec):
+    for kind, n, seed in [("T", 3 << 20, 99), ("R", 1 << 20, 1), ("P", 1 << 20, 2), ("T", 1000000, 1234),
+                          ("Z", 200001, 0), ("T", 65536 * 5 + 17, 4)]:
+        a = datagen.make(kind, n, seed)
+        comp, offs = codec.compress_tensor(to_dev(a), layout=snappy_amd.SINGLE)
+        want = oracle.compress(a.tobytes())
+        assert comp.cpu().numpy().tobytes() == want, (kind, n)
+        back = codec.decompress_tensor(comp, offs, n, layout=snappy_amd.SINGLE)
+        assert np.array_equal(back.cpu().numpy(), a)
+
+
+def test_streams_32k_device(codec, golden):
+    s = golden["streams_32k"]
+    a = datagen.make("T", s["spec"]["size"], s["spec"]["seed"])
+    comp, offs = codec.compress_tensor(to_dev(a), chunk=s["chunk"], layout=snappy_amd.STREAMS)
+    assert comp.numel() == s["out_len"]
+    assert sha(comp.cpu().numpy().tobytes()) == s["out_sha256"]
+    assert sha(offs.cpu().numpy().astype(np.uint64).tobytes()) == s["offsets_sha256"]
+    back = codec.decompress_tensor(comp, offs, a.size, chunk=s["chunk"], layout=snappy_amd.STREAMS)
+    assert np.array_equal(back.cpu().numpy(), a)
+
+
+@pytest.mark.parametrize("chunk", [1, 17, 4096, 32768, 65535, 65536])
+def test_streams_chunk_sizes(codec, chunk):
+    n = 300000 if chunk > 16 else 2000
+    a = datagen.make("T", n, chunk)
+    comp, offs = codec.compress_tensor(to_dev(a), chunk=chunk, layout=snappy_amd.STREAMS)
+    want, want_offs = oracle.compress_streams(a, chunk)
+    assert comp.cpu().numpy().tobytes() == want.tobytes()
+    assert np.array_equal(offs.cpu().numpy().astype(np.uint64), want_offs)
+    back = codec.decompress_tensor(comp, offs, n, chunk=chunk, layout=snappy_amd.STREAMS)
+    assert np.array_equal(back.cpu().numpy(), a)
+
+
+def test_reference_stream_index_and_decode(codec, golden):
+    # a reference-produced .snp has no block index: K5 builds it on the GPU
+    import torch
+    for name in ("text_3MiB", "license_1MiB", "random_1MiB", "edge_T_131073", "zeros_1MiB"):
+        e = next(x for x in golden["entries"] if x["name"] == name)
+        data = make_input(e["spec"])
+        stream = oracle.compress(data)  # == reference bytes (pinned by test_oracle)
+        assert sha(stream) == e["out_sha256"]
+        d = torch.from_numpy(np.frombuffer(stream, dtype=np.uint8).copy()).cuda()
+        n, offs = codec.index_tensor(d)
+        assert n == len(data)
+        back = codec.decompress_tensor(d, offs, n, layout=snappy_amd.SINGLE)
+        assert back.cpu().numpy().tobytes() == data
+
+
+def test_decoder_errors():
+    good = oracle.compress(datagen.make("T", 5000, 1).tobytes())
+    with pytest.raises(snappy_amd.SnappyError) as ei:
+        snappy_amd.decompress(good[:-5])
+    assert ei.value.code in (snappy_amd.ERR_TRUNCATED, snappy_amd.ERR_OVERRUN)
+    bad_off = bytes([8, 0]) + b"a" + bytes([(7 - 1) << 2 | 2, 9, 0])
+    with pytest.raises(snappy_amd.SnappyError) as ei:
+        snappy_amd.decompress(bad_off)
+    assert ei.value.code == snappy_amd.ERR_OFFSET
+    with pytest.raises(snappy_amd.SnappyError):
+        snappy_amd.decompress(b"\x80\x80\x80")
+
+
+def test_empty_and_tiny():
+    assert snappy_amd.compress(b"") == b""
+    assert snappy_amd.decompress(b"") == b""
+    for n in range(0, 40):
+        data = bytes((i * 37) % 5 for i in range(n))
+        out = snappy_amd.compress(data)
+        assert out == oracle.compress(data)
+        assert snappy_amd.decompress(out) == data
+
+
+def test_file_api_header_quirk():
+    import io
+    data = datagen.make("T", 100000, 3).tobytes()
+    fo = io.BytesIO()
+    snappy_amd.snappy_compress(io.BytesIO(data), 123456789, fo)  # header = the caller's input_size
+    assert fo.getvalue()[:4] == snappy_amd.varint_encode(123456789)
+    assert fo.getvalue()[4:] == oracle.compress(data)[3:]
+    fo2 = io.BytesIO()
+    snappy_amd.snappy_compress(io.BytesIO(b""), 10, fo2)  # empty read -> nothing written
+    assert fo2.getvalue() == b""
+
+
+def test_cli_round_trip(golden):
+    exe = os.path.join(ROOT, "lightweight-snappy_amd", "snappy")
+    e = next(x for x in golden["entries"] if x["name"] == "text_1000000")
+    data = make_input(e["spec"])
+    with tempfile.TemporaryDirectory() as d:
+        src, snp, dec = (os.path.join(d, x) for x in ("in", "in.snp", "in.dec"))
+        open(src, "wb").write(data)
+        subprocess.run([exe, "-c", "-r", src, snp], check=True, capture_output=True)
+        assert sha(open(snp, "rb").read()) == e["out_sha256"]
+        subprocess.run([exe, "-d", snp, dec], check=True, capture_output=True)
+        assert open(dec, "rb").read() == data
+        r = subprocess.run([exe, "-b", src, snp], capture_output=True)
+        assert r.returncode != 0
+
+
+def test_full_size_streams_1gib(codec):
+    """BASELINE.json configs[1] at full size: 1 GiB of 32 KiB text streams,
+    bit-exact against the (threaded) oracle and round-tripped on the GPU."""
+    import torch
+    n, chunk = 1 << 30, 32768
+    a = datagen.make("T", n, 1234)
+    comp, offs = codec.compress_tensor(to_dev(a), chunk=chunk, layout=snappy_amd.STREAMS)
+    want, want_offs = oracle.compress_streams(a, chunk, threads=16)
+    got = comp.cpu().numpy()
+    assert got.size == want.size
+    assert np.array_equal(offs.cpu().numpy().astype(np.uint64), want_offs)
+    assert np.array_equal(got, want)
+    back = codec.decompress_tensor(comp, offs, n, chunk=chunk, layout=snappy_amd.STREAMS)
+    assert torch.equal(back, to_dev(a))
+
+
+@pytest.mark.parametrize("kind,seed", [("R", 1), ("P", 2)])
+def test_full_size_extremes_1gib(codec, kind, seed):
+    """configs[2]: 1 GiB random (all-literal) and 64-byte repeat (all-copy),
+    one SINGLE stream each."""
+    import torch
+    n = 1 << 30
+    a = datagen.make(kind, n, seed)
+    comp, offs = codec.compress_tensor(to_dev(a), layout=snappy_amd.SINGLE)
+    if kind == "R":
+        assert 0.9999 < n / comp.numel() < 1.0  # ~every block one 65,536-byte literal
+    else:
+        assert 20.0 < n / comp.numel() < 21.5
+    # bit-exact on a 64 MiB prefix stream + index-consistency on the whole
+    pre = a[: 64 << 20]
+    cpre, _ = codec.compress_tensor(to_dev(pre), layout=snappy_amd.SINGLE)
+    assert cpre.cpu().numpy().tobytes() == oracle.compress(pre.tobytes())
+    back = codec.decompress_tensor(comp, offs, n, layout=snappy_amd.SINGLE)
+    assert torch.equal(back, to_dev(a))

@@ -22,6 +22,10 @@ struct snappy_amd_ctx {
     size_t scratch_cap = 0;
     uint32_t *sizes = nullptr;
     size_t sizes_cap = 0;
+    uint2 *tokens = nullptr;
+    size_t tokens_cap = 0;
+    uint32_t *ntok = nullptr;
+    size_t ntok_cap = 0;
     int32_t *status = nullptr;
     size_t status_cap = 0;
     uint64_t *total = nullptr;      // device u64
@@ -53,7 +57,7 @@ static int grow(void **ptr, size_t *cap, size_t need)
     return SNAPPY_AMD_OK;
 }
 
-static size_t k1_lds_bytes(uint32_t unit) { return 8192 + ((unit + 15) & ~15u) + 32; }
+static size_t k1_lds_bytes(uint32_t unit) { return 8192 + ((unit + 15) & ~15u); }
 static size_t k4_lds_bytes(uint32_t unit, uint32_t comp_cap) { return ((unit + 15) & ~15u) + 16 + comp_cap + 32; }
 
 extern "C" {
@@ -90,7 +94,7 @@ void snappy_amd_destroy(snappy_amd_ctx *c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void *bufs[] = {c->scratch, c->sizes, c->status, c->total, c->k5res, c->d_a, c->d_b, c->d_idx};
+    void *bufs[] = {c->scratch, c->sizes, c->tokens, c->ntok, c->status, c->total, c->k5res, c->d_a, c->d_b, c->d_idx};
     for (void *b : bufs) if (b) (void)hipFree(b);
     if (c->h_total) (void)hipHostFree(c->h_total);
     if (c->h_status) (void)hipHostFree(c->h_status);
@@ -170,8 +174,32 @@ static int compress_impl(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t
         return SNAPPY_AMD_OK;
     }
     const size_t units = (n + unit - 1) / unit;
-    const uint64_t stride = unit_stride(unit);
     int rc;
+    if (unit <= SNAPPY_K1R_MAX_UNIT && !getenv("SNAPPY_AMD_FORCE_LDS_K1")) {
+        // register-resident match finder -> tokens; scan; emit in place
+        const uint32_t tok_cap = unit / 4 + 2;
+        if ((rc = grow(reinterpret_cast<void **>(&c->tokens), &c->tokens_cap,
+                       units * tok_cap * sizeof(uint2) + units * 4 * sizeof(uint64_t))))
+            return rc;
+        if ((rc = grow(reinterpret_cast<void **>(&c->ntok), &c->ntok_cap, units * sizeof(uint32_t)))) return rc;
+        if ((rc = grow(reinterpret_cast<void **>(&c->sizes), &c->sizes_cap, units * sizeof(uint32_t)))) return rc;
+        const uint32_t hm = hdr_mode_of(layout, flags);
+        if (c->timing) (void)hipEventRecord(c->ev[0], c->stream);
+        hipLaunchKernelGGL(k1r_match_units, dim3((uint32_t)units), dim3(64), 0, c->stream,
+                           static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens, tok_cap,
+                           c->ntok, c->sizes);
+        HIP_OK(hipGetLastError());
+        if (c->timing) (void)hipEventRecord(c->ev[1], c->stream);
+        hipLaunchKernelGGL(k3_scan, dim3(1), dim3(1024), 0, c->stream, c->sizes, (uint64_t)units, d_offsets, c->total);
+        hipLaunchKernelGGL(k2_emit_units, dim3((uint32_t)units), dim3(64), 0, c->stream,
+                           static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens, tok_cap,
+                           c->ntok, d_offsets, static_cast<uint8_t *>(d_out));
+        HIP_OK(hipGetLastError());
+        if (c->timing) (void)hipEventRecord(c->ev[2], c->stream);
+        goto done;
+    }
+    {
+    const uint64_t stride = unit_stride(unit);
     if ((rc = grow(reinterpret_cast<void **>(&c->scratch), &c->scratch_cap, units * stride))) return rc;
     if ((rc = grow(reinterpret_cast<void **>(&c->sizes), &c->sizes_cap, units * sizeof(uint32_t)))) return rc;
     const uint32_t vec_ok = ((reinterpret_cast<uintptr_t>(d_in) | unit) & 15) == 0;
@@ -187,6 +215,8 @@ static int compress_impl(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t
                        d_offsets, static_cast<uint8_t *>(d_out));
     HIP_OK(hipGetLastError());
     if (c->timing) (void)hipEventRecord(c->ev[2], c->stream);
+    }
+done:
     if (out_len) {
         HIP_OK(hipMemcpyAsync(c->h_total, c->total, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
         HIP_OK(hipStreamSynchronize(c->stream));

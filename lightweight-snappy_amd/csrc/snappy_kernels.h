@@ -34,6 +34,16 @@ __host__ __device__ inline uint64_t unit_stride(uint32_t unit)
 __global__ void k1_compress_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit, uint32_t hdr_mode,
                                   uint64_t header_value, uint32_t vec_ok, uint8_t *__restrict__ scratch,
                                   uint64_t stride, uint32_t *__restrict__ sizes);
+__global__ void k1r_match_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit, uint32_t hdr_mode,
+                                uint64_t header_value, uint2 *__restrict__ tokens, uint32_t tok_cap,
+                                uint32_t *__restrict__ ntok_out, uint32_t *__restrict__ sizes);
+__global__ void k2_emit_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit, uint32_t hdr_mode,
+                              uint64_t header_value, const uint2 *__restrict__ tokens, uint32_t tok_cap,
+                              const uint32_t *__restrict__ ntok, const uint64_t *__restrict__ offsets,
+                              uint8_t *__restrict__ out);
+// register-resident K1r handles units up to this size (128 VGPRs x 64 lanes x 4 B)
+#define SNAPPY_K1R_MAX_UNIT 32768u
+
 __global__ void k3_scan(const uint32_t *__restrict__ sizes, uint64_t count, uint64_t *__restrict__ offsets,
                         uint64_t *__restrict__ total);
 __global__ void k3_gather(const uint8_t *__restrict__ scratch, uint64_t stride, const uint32_t *__restrict__ sizes,

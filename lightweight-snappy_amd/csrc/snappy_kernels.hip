@@ -81,8 +81,24 @@ __device__ __forceinline__ uint32_t emit_literal(uint8_t *ob, uint32_t o, const 
 
 // Copy split 64/60 (src/snappy_compression.c:153-165) and piece encoding
 // (:131-145): copy-1 iff len < 12 && off < 2048, else copy-2; never copy-4.
+__device__ __forceinline__ uint32_t piece_bytes(uint32_t len, uint32_t off, uint32_t *nb)
+{
+    if (len < 12 && off < 2048) {
+        *nb = 2;
+        return ((((off >> 8) << 5) + ((len - 4) << 2) + 1) & 0xFF) | ((off & 0xFF) << 8);
+    }
+    *nb = 3;
+    return (((len - 1) << 2) | 2) | ((off & 0xFF) << 8) | (((off >> 8) & 0xFF) << 16);
+}
+
 __device__ __forceinline__ uint32_t emit_copy(uint8_t *ob, uint32_t o, uint32_t len, uint32_t off, uint32_t lane)
 {
+    if (len <= 64) {  // one piece: the common case
+        uint32_t nb;
+        const uint32_t v = piece_bytes(len, off, &nb);
+        if (lane < nb) ob[o + lane] = (uint8_t)(v >> (8 * lane));
+        return o + nb;
+    }
     const uint32_t n64 = len > 68 ? (len - 68 + 63) >> 6 : 0;
     const uint32_t rem = len - 64 * n64;
     const uint32_t has60 = rem > 64 ? 1u : 0u;
@@ -90,14 +106,8 @@ __device__ __forceinline__ uint32_t emit_copy(uint8_t *ob, uint32_t o, uint32_t 
     const uint32_t offb = ((off & 0xFF) << 8) | (((off >> 8) & 0xFF) << 16);
     const uint32_t c64 = 0xFEu | offb;  // ((64-1)<<2)|2
     const uint32_t c60 = 0xEEu | offb;  // ((60-1)<<2)|2
-    uint32_t lastb, lastl;
-    if (last < 12 && off < 2048) {
-        lastl = 2;
-        lastb = ((((off >> 8) << 5) + ((last - 4) << 2) + 1) & 0xFF) | ((off & 0xFF) << 8);
-    } else {
-        lastl = 3;
-        lastb = (((last - 1) << 2) | 2) | offb;
-    }
+    uint32_t lastl;
+    const uint32_t lastb = piece_bytes(last, off, &lastl);
     const uint32_t body = 3 * (n64 + has60);
     const uint32_t total = body + lastl;
     for (uint32_t b = 0; b < total; b += 64) {
@@ -117,11 +127,78 @@ __device__ __forceinline__ uint32_t emit_copy(uint8_t *ob, uint32_t o, uint32_t 
     return o + total;
 }
 
+// Probe position of the k-th consecutive miss after (p, skip):
+// p_k = p + sum_{j<k} ((skip + j) >> 5) = p + F(skip + k) - F(skip), with
+// F(m) = sum_{i<m} (i >> 5) = 16 q (q - 1) + (m & 31) q, q = m >> 5.
+__device__ __forceinline__ uint32_t skipsum(uint32_t m)
+{
+    const uint32_t q = m >> 5;
+    return 16 * q * (q - 1) + (m & 31) * q;
+}
+
+// row_shr:N inside 16-lane DPP rows; lanes with no source get 0xFFFFFFFF
+// (never equal to a 12-bit hash or to a position + 1).
+template <int N>
+__device__ __forceinline__ uint32_t shr(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)v, 0x110 + N, 0xF, 0xF, false);
+}
+
+// Lane k (< W) conflicts with an earlier lane j of the window when its probe
+// would read a slot j writes (h_k in {h_j, a_j}) or when the two lanes would
+// write different positions into one slot in the same LDS instruction
+// (a_k in {a_j} or a_k == h_j with p_j != p_k - 1).  Only j = k - 1 can have
+// p_j == p_k - 1 (when its step is 1): `dup` carries that fact.
+template <int N>
+__device__ __forceinline__ bool conflict_step(uint32_t h, uint32_t a, bool dup)
+{
+    const uint32_t hs = shr<N>(h), as = shr<N>(a);
+    if constexpr (N == 1) return (h == hs) | (h == as) | (a == as) | ((a == hs) & !dup);
+    else return (h == hs) | (h == as) | (a == as) | (a == hs);
+}
+
+template <int W>
+__device__ __forceinline__ bool window_conflict(uint32_t h, uint32_t a, bool dup)
+{
+    bool c = false;
+    if constexpr (W > 1) c |= conflict_step<1>(h, a, dup);
+    if constexpr (W > 2) c |= conflict_step<2>(h, a, dup);
+    if constexpr (W > 3) c |= conflict_step<3>(h, a, dup);
+    if constexpr (W > 4) {
+        c |= conflict_step<4>(h, a, dup);
+        c |= conflict_step<5>(h, a, dup);
+        c |= conflict_step<6>(h, a, dup);
+        c |= conflict_step<7>(h, a, dup);
+    }
+    if constexpr (W > 8) {
+        c |= conflict_step<8>(h, a, dup);
+        c |= conflict_step<9>(h, a, dup);
+        c |= conflict_step<10>(h, a, dup);
+        c |= conflict_step<11>(h, a, dup);
+        c |= conflict_step<12>(h, a, dup);
+        c |= conflict_step<13>(h, a, dup);
+        c |= conflict_step<14>(h, a, dup);
+        c |= conflict_step<15>(h, a, dup);
+    }
+    return c;
+}
+
 // ---------------------------------------------------------------------------
-// K1: one wave per unit.  All control state is wave-uniform (SGPRs); the
-// lanes cooperate on staging, match extension (64 bytes per ballot) and
-// element emission.
+// K1: one wave per unit.  Control state (p, skip, literal start, output
+// cursor) is wave-uniform.  Each round speculates that the next W probes all
+// miss: lane k computes probe k's position in closed form, hashes, reads its
+// table slot and candidate bytes; a ballot finds the first lane that matches,
+// conflicts with an earlier lane of the window, or is past the block end.
+// Lanes before it are exact misses (their inserts are applied, collision-free
+// by construction); the match, if any, is exact too.  This reproduces the
+// reference's serial probe/insert order bit for bit while paying the LDS
+// round trips once per window instead of once per probe.
 // ---------------------------------------------------------------------------
+#ifndef SNAPPY_K1_WINDOW
+#define SNAPPY_K1_WINDOW 8
+#endif
+constexpr int kWin = SNAPPY_K1_WINDOW;
+
 __global__ __launch_bounds__(64) void k1_compress_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
                                                         uint32_t hdr_mode, uint64_t header_value, uint32_t vec_ok,
                                                         uint8_t *__restrict__ scratch, uint64_t stride,
@@ -147,8 +224,7 @@ __global__ __launch_bounds__(64) void k1_compress_units(const uint8_t *__restric
     } else {
         for (uint32_t i = lane; i < L; i += 64) inb[i] = src[i];
     }
-    if (lane < 16) inb[L + lane] = 0;
-    for (uint32_t i = lane; i < kTable / 2; i += 64) lds[i] = 0;
+    for (uint32_t i = lane * 4; i < kTable / 2; i += 256) *reinterpret_cast<u32x4 *>(lds + i) = u32x4{0, 0, 0, 0};
     __syncthreads();
 
     uint8_t *ob = scratch + (uint64_t)u * stride;
@@ -163,35 +239,386 @@ __global__ __launch_bounds__(64) void k1_compress_units(const uint8_t *__restric
 
     uint32_t p = 1, skip = 33, lit = 0;  // start_new_literal + append_literal
     while (!(L - p < (skip >> 5) + 15)) {  // is_block_end :229-232
-        const uint32_t cur = rfl(be32_at(inw, p));
+        // ---- speculative window: lane k = k-th probe if all earlier miss
+        const uint32_t sk = skip + lane;
+        const uint32_t pk = p + skipsum(sk) - skipsum(skip);
+        const bool valid = lane < (uint32_t)kWin && (int32_t)(L - pk) >= (int32_t)((sk >> 5) + 15);
+        const uint32_t q = valid ? pk - 1 : 0;
+        const uint32_t lo = inw[q >> 2], hi = inw[(q >> 2) + 1];
+        const uint64_t w8 = ((uint64_t)hi << 32) | lo;
+        const uint32_t prev = __builtin_bswap32((uint32_t)(w8 >> (8 * (q & 3))));
+        const uint32_t cur = __builtin_bswap32((uint32_t)(w8 >> (8 * (q & 3) + 8)));
         const uint32_t h = (cur * kMul) >> shift;
-        const uint32_t cand = rfl(table[h]);
-        const uint32_t cv = rfl(be32_at(inw, cand));
-        if (cv == cur) {  // found_match :259-265
-            if (p > lit) o = emit_literal(ob, o, inb, lit, p - lit, lane);
-            skip = 32;
+        const uint32_t a = (prev * kMul) >> shift;
+        const uint32_t cand = table[h];
+        // the previous lane's step was 1 iff its skip counter was < 64
+        const bool dup = lane > 0 && ((sk - 1) >> 5) == 1;
+        const bool conflict = window_conflict<kWin>(h, a, dup);  // VALU under the table read
+        const bool hit = be32_at(inw, cand) == cur;  // found_match :259-265
+        const uint64_t stop = __ballot(!valid || conflict || hit);
+        const uint32_t f = (uint32_t)__builtin_ctzll(stop);  // < kWin + 1
+        // lanes before f are exact misses: update_hash_table :303-307
+        if (lane < f) table[a] = (uint16_t)(pk - 1);
+        if (lane < f) table[h] = (uint16_t)pk;
+        const uint64_t match = __ballot(valid && !conflict && hit);
+        if ((match >> f) & 1) {
+            const uint32_t pf = __builtin_amdgcn_readlane(pk, f);
+            const uint32_t cf = __builtin_amdgcn_readlane(cand, f);
+            const uint32_t hf = __builtin_amdgcn_readlane(h, f);
+            if (pf > lit) o = emit_literal(ob, o, inb, lit, pf - lit, lane);
             uint32_t len = 4;  // find_copy_length :61-72, limit = block end
             for (;;) {
-                const uint32_t q = p + len + lane;
-                const bool ok = q < L && inb[q] == inb[cand + len + lane];
+                const uint32_t qq = pf + len + lane;
+                const bool ok = qq < L && inb[qq] == inb[cf + len + lane];
                 const uint64_t bad = __ballot(!ok);
                 if (bad) { len += (uint32_t)__builtin_ctzll(bad); break; }
                 len += 64;
             }
-            o = emit_copy(ob, o, len, p - cand, lane);
-            table[h] = (uint16_t)p;  // emit_copy :328
-            p += len;
+            o = emit_copy(ob, o, len, pf - cf, lane);
+            if (lane == 0) table[hf] = (uint16_t)pf;  // emit_copy :328
+            skip = 32;
+            p = pf + len;
             lit = p;
-        } else {  // update_hash_table :303-307, append_literal :283-287
-            const uint32_t prev = rfl(be32_at(inw, p - 1));
-            table[(prev * kMul) >> shift] = (uint16_t)(p - 1);
-            table[h] = (uint16_t)p;
-            p += skip >> 5;
-            skip++;
+        } else {
+            // f misses consumed; f stops at a conflict (retried exactly as the
+            // next window's lane 0) or at the block end
+            p = p + skipsum(skip + f) - skipsum(skip);
+            skip += f;
         }
     }
     if (L > lit) o = emit_literal(ob, o, inb, lit, L - lit, lane);  // exhaust_input + emit_literal
     if (lane == 0) sizes[u] = o;
+}
+
+// ---------------------------------------------------------------------------
+// K1r: register-resident match finder for units <= 32 KiB (the STREAMS
+// layout of BASELINE.json configs[1]).  The unit lives in 128 VGPRs of its
+// wave (dword d = 64 r + lane, stored big-endian so the reference's BE32
+// loads are SALU funnel shifts), the u16 hash table alone in LDS (8 KiB).
+// 168 VGPRs -> 3 waves per SIMD, 12 units in flight per CU (the LDS-staged
+// K1 fits 4).  Uniform positions read a VGPR by s_set_gpr_idx + v_readlane;
+// the serial probe chain of snappy_compression.c:384-403 runs in SGPRs with
+// one LDS round trip (the table) per probe.  Output is a token list
+// (pos | len << 16, offset) plus the unit's exact encoded size; K2 writes the
+// bytes once K3 has placed every unit.
+// ---------------------------------------------------------------------------
+typedef uint32_t v32 __attribute__((ext_vector_type(32)));
+
+// The unit's 128 VGPRs are four v32 locals g0..g3 of the kernel, pinned to
+// v2..v129 by the asm constraints below so that one s_set_gpr_idx_on +
+// v_mov reads VGPR v[2 + r] for a wave-uniform r (a C++ switch over the four
+// vectors compiles to a branch tree, and passing them by reference or in a
+// struct sends them to scratch).
+#define REG_OF(r)                                                                              \
+    ({                                                                                         \
+        uint32_t _v;                                                                           \
+        asm volatile("s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\tv_mov_b32 %0, v2\n\ts_set_gpr_idx_off" \
+                     : "=&v"(_v)                                                               \
+                     : "s"((uint32_t)(r)), "{v[2:33]}"(g0), "{v[34:65]}"(g1), "{v[66:97]}"(g2),     \
+                       "{v[98:129]}"(g3));                                                     \
+        _v;                                                                                    \
+    })
+
+// big-endian dwords d, d+1 of the unit as one u64 (d wave-uniform)
+#define BE_PAIR(dd)                                                                          \
+    ({                                                                                       \
+        const uint32_t _d = (dd);                                                            \
+        const uint32_t _v = REG_OF(_d >> 6);                                                 \
+        const uint32_t _hi = __builtin_amdgcn_readlane(_v, _d & 63);                         \
+        uint32_t _lo;                                                                        \
+        if ((_d & 63) != 63) _lo = __builtin_amdgcn_readlane(_v, (_d & 63) + 1);             \
+        else _lo = _d + 1 < 8192 ? __builtin_amdgcn_readlane(REG_OF((_d >> 6) + 1), 0) : 0; \
+        ((uint64_t)_hi << 32) | _lo;                                                         \
+    })
+
+// BE32 load at byte q (src/snappy_compression.c:239-241)
+#define BE32_REG(qq)                                                        \
+    ({                                                                      \
+        const uint32_t _q = (qq);                                           \
+        (uint32_t)((BE_PAIR(_q >> 2) << (8 * (_q & 3))) >> 32);             \
+    })
+
+// 8 bytes at q in memory order (first byte in the top bits)
+#define BE64_REG(qq)                                                        \
+    ({                                                                      \
+        const uint32_t _q8 = (qq);                                          \
+        const uint32_t _s8 = 8 * (_q8 & 3);                                 \
+        const uint64_t _a8 = BE_PAIR(_q8 >> 2);                             \
+        uint64_t _r8 = _a8;                                                 \
+        if (_s8) {                                                          \
+            const uint32_t _c8 = (uint32_t)(BE_PAIR((_q8 >> 2) + 2) >> 32); \
+            _r8 = (_a8 << _s8) | (_c8 >> (32 - _s8));                       \
+        }                                                                   \
+        _r8;                                                                \
+    })
+
+// per-lane BE dword at byte q + 4*lane (q uniform), for wave-parallel compares
+#define BE32_LANES(qq)                                                                               \
+    ({                                                                                               \
+        const uint32_t _ql = (qq);                                                                   \
+        const uint32_t _d0 = _ql >> 2, _r0 = _d0 >> 6;                                              \
+        const uint32_t _v0 = REG_OF(_r0);                                                            \
+        const uint32_t _v1 = _r0 + 1 < 128 ? REG_OF(_r0 + 1) : 0;                                    \
+        const uint32_t _e = (_d0 & 63) + lane, _f = _e + 1;                                          \
+        const uint32_t _a0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_e & 63) << 2), (int)_v0); \
+        const uint32_t _a1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_e & 63) << 2), (int)_v1); \
+        const uint32_t _b0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_f & 63) << 2), (int)_v0); \
+        const uint32_t _b1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_f & 63) << 2), (int)_v1); \
+        const uint32_t _hi = _e < 64 ? _a0 : _a1, _lo = _f < 64 ? _b0 : _b1;                        \
+        const uint32_t _s = 8 * (_ql & 3);                                                           \
+        _s ? (_hi << _s) | (_lo >> (32 - _s)) : _hi;                                                 \
+    })
+
+__device__ __forceinline__ uint32_t varint_len(uint64_t v)
+{
+    uint32_t len = 1;
+    while (v >= 128) { v >>= 7; len++; }
+    return len;
+}
+
+// encoded size of a literal of n bytes (src/snappy_compression.c:95-120)
+__device__ __forceinline__ uint32_t literal_bytes(uint32_t n)
+{
+    return n + (n <= 60 ? 1 : (n <= 256 ? 2 : 3));
+}
+
+// encoded size of a copy (src/snappy_compression.c:131-165)
+__device__ __forceinline__ uint32_t copy_bytes(uint32_t len, uint32_t off)
+{
+    const uint32_t n64 = len > 68 ? (len - 68 + 63) >> 6 : 0;
+    const uint32_t rem = len - 64 * n64;
+    const uint32_t has60 = rem > 64 ? 1u : 0u;
+    const uint32_t last = has60 ? rem - 60 : rem;
+    return 3 * (n64 + has60) + ((last < 12 && off < 2048) ? 2 : 3);
+}
+
+__global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
+                                                          uint32_t hdr_mode, uint64_t header_value,
+                                                          uint2 *__restrict__ tokens, uint32_t tok_cap,
+                                                          uint32_t *__restrict__ ntok_out,
+                                                          uint32_t *__restrict__ sizes)
+{
+    __shared__ uint16_t table[kTable];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t u = blockIdx.x;
+    const uint64_t base = (uint64_t)u * unit;
+    const uint32_t L = (uint32_t)((n - base) < unit ? (n - base) : unit);
+    const uint8_t *src = in + base;
+#ifdef SNAPPY_K1R_STATS
+    const uint64_t t_start = clock64();
+#endif
+
+    // unit -> VGPRs, dword d = 64 r + lane, big-endian, zero past the end
+    v32 g0, g1, g2, g3;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(src) & 3) == 0);
+#pragma unroll
+    for (int i = 0; i < 128; i++) {
+        const uint32_t b = 4 * (64 * i + lane);
+        uint32_t w = 0;
+        if (b + 4 <= L && aligned) {
+            w = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(src + b));
+        } else {
+            for (uint32_t k = 0; k < 4; k++)
+                if (b + k < L) w |= (uint32_t)src[b + k] << (8 * k);
+        }
+        w = __builtin_bswap32(w);
+        if (i < 32) g0[i] = w;
+        else if (i < 64) g1[i - 32] = w;
+        else if (i < 96) g2[i - 64] = w;
+        else g3[i - 96] = w;
+    }
+    for (uint32_t i = lane; i < kTable / 2; i += 64) reinterpret_cast<uint32_t *>(table)[i] = 0;
+    __syncthreads();
+
+    uint32_t enc = 0;
+    if (hdr_mode == SNAPPY_HDR_EVERY_UNIT) enc = varint_len(L);
+    else if (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0) enc = varint_len(header_value);
+
+    uint32_t T = 256, lg = 8;  // set_htable_size :198-204
+    while (T < kTable && T < L) { T <<= 1; lg++; }
+    const uint32_t shift = 32 - lg;
+
+    uint2 *tok = tokens + (uint64_t)u * tok_cap;
+    uint32_t tka = 0, tkb = 0;  // 64 pending tokens, lane t holds token t
+    uint32_t nt = 0;
+
+#ifdef SNAPPY_K1R_STATS
+    const uint64_t t_loop = clock64();
+    uint32_t n_probe = 0, n_match = 0;
+#endif
+    uint32_t p = 1, skip = 33, lit = 0;
+    while (!(L - p < (skip >> 5) + 15)) {  // is_block_end :229-232
+#ifdef SNAPPY_K1R_STATS
+        n_probe++;
+#endif
+        const uint64_t w = BE_PAIR((p - 1) >> 2) << (8 * ((p - 1) & 3));
+        const uint32_t prev = (uint32_t)(w >> 32);
+        const uint32_t cur = (uint32_t)(w >> 24);
+        const uint32_t h = (cur * kMul) >> shift;
+        const uint32_t cand = __builtin_amdgcn_readfirstlane(table[h]);
+        if (BE32_REG(cand) == cur) {  // found_match :259-265
+            // find_copy_length :61-72: 8 bytes by SALU, then 256 per wave pass
+            uint32_t len = 4;
+            const uint64_t x = BE64_REG(p + 4) ^ BE64_REG(cand + 4);
+            if (x) {
+                len += (uint32_t)__builtin_clzll(x) >> 3;
+            } else {
+                len = 12;
+                for (;;) {
+                    if (p + len >= L) break;
+                    const uint32_t y = BE32_LANES(p + len) ^ BE32_LANES(cand + len);
+                    const uint64_t bad = __ballot(y != 0);
+                    if (bad) {
+                        const uint32_t m = (uint32_t)__builtin_ctzll(bad);
+                        const uint32_t ym = __builtin_amdgcn_readlane(y, m);
+                        len += 4 * m + ((uint32_t)__builtin_clz(ym) >> 3);
+                        break;
+                    }
+                    len += 256;
+                }
+            }
+            if (len > L - p) len = L - p;  // the compare never runs past the block
+#ifdef SNAPPY_K1R_STATS
+            n_match++;
+#endif
+            const uint32_t off = p - cand;
+            if (p > lit) enc += literal_bytes(p - lit);
+            enc += copy_bytes(len, off);
+            if (lane == (nt & 63)) {
+                tka = p | (len << 16);
+                tkb = off;
+            }
+            nt++;
+            if ((nt & 63) == 0) tok[nt - 64 + lane] = make_uint2(tka, tkb);
+            if (lane == 0) table[h] = (uint16_t)p;  // emit_copy :328
+            skip = 32;
+            p += len;
+            lit = p;
+        } else {  // update_hash_table :303-307, append_literal :283-287
+            if (lane == 0) {
+                table[(prev * kMul) >> shift] = (uint16_t)(p - 1);
+                table[h] = (uint16_t)p;
+            }
+            p += skip >> 5;
+            skip++;
+        }
+    }
+    if (L > lit) enc += literal_bytes(L - lit);
+    if (lane < (nt & 63)) tok[(nt & ~63u) + lane] = make_uint2(tka, tkb);
+    if (lane == 0) {
+        ntok_out[u] = nt;
+        sizes[u] = enc;
+    }
+#ifdef SNAPPY_K1R_STATS
+    if (lane == 0) {
+        // debug side channel: 4 u64 per unit after the token area of unit 0..
+        uint64_t *st = reinterpret_cast<uint64_t *>(tokens + (uint64_t)gridDim.x * tok_cap) + 4 * (uint64_t)u;
+        st[0] = clock64() - t_loop;
+        st[1] = t_loop - t_start;
+        st[2] = n_probe;
+        st[3] = n_match;
+    }
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// K2: token list -> Snappy bytes at the unit's final offset (after K3's scan),
+// one wave per unit, one token per lane: literal header + literal bytes (read
+// from the input) + copy pieces, exactly as write_literal / write_copy lay
+// them out (src/snappy_compression.c:95-165).  The last pseudo-token carries
+// the tail literal.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, uint32_t *total)
+{
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    *total = (uint32_t)__shfl((int)x, 63, 64);
+    return x - v;
+}
+
+__device__ __forceinline__ void put_copy(uint8_t *o, uint32_t len, uint32_t off)
+{
+    while (len > 68) {
+        o[0] = 0xFE; o[1] = (uint8_t)off; o[2] = (uint8_t)(off >> 8);
+        o += 3; len -= 64;
+    }
+    if (len > 64) {
+        o[0] = 0xEE; o[1] = (uint8_t)off; o[2] = (uint8_t)(off >> 8);
+        o += 3; len -= 60;
+    }
+    if (len < 12 && off < 2048) {
+        o[0] = (uint8_t)((((off >> 8) << 5) + ((len - 4) << 2) + 1));
+        o[1] = (uint8_t)off;
+    } else {
+        o[0] = (uint8_t)(((len - 1) << 2) | 2); o[1] = (uint8_t)off; o[2] = (uint8_t)(off >> 8);
+    }
+}
+
+__global__ __launch_bounds__(64) void k2_emit_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
+                                                    uint32_t hdr_mode, uint64_t header_value,
+                                                    const uint2 *__restrict__ tokens, uint32_t tok_cap,
+                                                    const uint32_t *__restrict__ ntok,
+                                                    const uint64_t *__restrict__ offsets, uint8_t *__restrict__ out)
+{
+    const uint32_t lane = threadIdx.x;
+    const uint32_t u = blockIdx.x;
+    const uint64_t base = (uint64_t)u * unit;
+    const uint32_t L = (uint32_t)((n - base) < unit ? (n - base) : unit);
+    const uint8_t *src = in + base;
+    uint8_t *dst = out + offsets[u];
+    uint32_t o = 0;
+    if (hdr_mode == SNAPPY_HDR_EVERY_UNIT) o = varint_put(L, dst, lane);
+    else if (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0) o = varint_put(header_value, dst, lane);
+
+    const uint2 *tok = tokens + (uint64_t)u * tok_cap;
+    const uint32_t nt = ntok[u];
+    uint32_t carry = 0;  // end of the previous token = start of this literal
+    for (uint32_t c = 0; c <= nt; c += 64) {
+        const uint32_t t = c + lane;
+        uint32_t pos = L, len = 0, off = 0;  // pseudo-token: tail literal
+        bool live = t <= nt;
+        if (t < nt) {
+            const uint2 k = tok[t];
+            pos = k.x & 0xFFFF;
+            len = k.x >> 16;
+            off = k.y;
+            if (len == 0) len = 65536;  // unreachable for units <= 32 KiB
+        }
+        const uint32_t end = pos + len;
+        uint32_t prev_end = (uint32_t)__shfl_up((int)end, 1, 64);
+        if (lane == 0) prev_end = carry;
+        const uint32_t litn = live ? pos - prev_end : 0;
+        const uint32_t hl = litn ? (litn <= 60 ? 1 : (litn <= 256 ? 2 : 3)) : 0;
+        const uint32_t cb = (live && len) ? copy_bytes(len, off) : 0;
+        uint32_t total;
+        const uint32_t my = o + wave_excl_scan(hl + litn + cb, lane, &total);
+        if (live) {
+            uint8_t *w = dst + my;
+            if (hl == 1) w[0] = (uint8_t)((litn - 1) << 2);
+            else if (hl == 2) { w[0] = 60 << 2; w[1] = (uint8_t)(litn - 1); }
+            else if (hl == 3) { w[0] = 61 << 2; w[1] = (uint8_t)(litn - 1); w[2] = (uint8_t)((litn - 1) >> 8); }
+            if (litn <= 16) {
+                for (uint32_t j = 0; j < litn; j++) w[hl + j] = src[prev_end + j];
+            }
+            if (len) put_copy(w + hl + litn, len, off);
+        }
+        // long literals: the whole wave copies each one
+        uint64_t longs = __ballot(live && litn > 16);
+        while (longs) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(longs);
+            longs &= longs - 1;
+            const uint32_t ln = __builtin_amdgcn_readlane(litn, k);
+            const uint32_t s0 = __builtin_amdgcn_readlane(prev_end, k);
+            const uint32_t d0 = __builtin_amdgcn_readlane(my + hl, k);
+            for (uint32_t j = lane; j < ln; j += 64) dst[d0 + j] = src[s0 + j];
+        }
+        carry = (uint32_t)__shfl((int)end, 63, 64);
+        o += total;
+    }
 }
 
 // ---------------------------------------------------------------------------

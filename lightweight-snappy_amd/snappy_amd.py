@@ -21,7 +21,7 @@ except Exception:  # pragma: no cover - torch is always present in this image
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsnappy_amd.so")
+LIB_PATH = os.environ.get("SNAPPY_AMD_LIB") or os.path.join(HERE, "libsnappy_amd.so")
 
 OK = 0
 ERR_ARG = -1

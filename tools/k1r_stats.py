@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""Run the SNAPPY_K1R_STATS variant and summarise per-unit cycles/probe."""
+import ctypes, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "lightweight-snappy_amd"))
+os.environ["SNAPPY_AMD_LIB"] = os.path.join(ROOT, "lightweight-snappy_amd", "variants", "libsnappy_amd_stats.so")
+import numpy as np, torch
+import datagen, snappy_amd
+kind = sys.argv[1] if len(sys.argv) > 1 else "T"
+n, chunk = 256 << 20, 32768
+a = datagen.make(kind, n, 1234 if kind == "T" else 1)
+x = torch.from_numpy(a).cuda()
+c = snappy_amd.Codec(0)
+comp, offs = c.compress_tensor(x, chunk=chunk, layout=snappy_amd.STREAMS)
+comp, offs = c.compress_tensor(x, chunk=chunk, layout=snappy_amd.STREAMS)
+torch.cuda.synchronize()
+lib = snappy_amd.lib()
+# the context's token buffer pointer is private: re-run through a probe kernel is overkill; read via hipMemcpy of ctx->tokens
+class Ctx(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("own", ctypes.c_void_p), ("stream", ctypes.c_void_p), ("scratch", ctypes.c_void_p),
+                ("scratch_cap", ctypes.c_size_t), ("sizes", ctypes.c_void_p), ("sizes_cap", ctypes.c_size_t),
+                ("tokens", ctypes.c_void_p), ("tokens_cap", ctypes.c_size_t)]
+ctx = ctypes.cast(c._h, ctypes.POINTER(Ctx)).contents
+units = n // chunk
+tok_cap = chunk // 4 + 2
+hip = ctypes.CDLL("libamdhip64.so")
+buf = np.empty(units * 4, dtype=np.uint64)
+rc = hip.hipMemcpy(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ctx.tokens + units * tok_cap * 8), ctypes.c_size_t(buf.nbytes), 2)
+st = buf.reshape(units, 4)
+loop, start, probes, matches = st[:, 0], st[:, 1], st[:, 2], st[:, 3]
+print(f"{kind}: units {units} probes/unit {probes.mean():.0f} matches/unit {matches.mean():.0f}")
+print(f"loop cycles/unit {loop.mean():.0f}  start cycles/unit {start.mean():.0f}  cycles/probe {loop.sum() / probes.sum():.1f}")

@@ -292,81 +292,79 @@ __global__ __launch_bounds__(64) void k1_compress_units(const uint8_t *__restric
 
 // ---------------------------------------------------------------------------
 // K1r: register-resident match finder for units <= 32 KiB (the STREAMS
-// layout of BASELINE.json configs[1]).  The unit lives in 128 VGPRs of its
-// wave (dword d = 64 r + lane, stored big-endian so the reference's BE32
-// loads are SALU funnel shifts), the u16 hash table alone in LDS (8 KiB).
-// 168 VGPRs -> 3 waves per SIMD, 12 units in flight per CU (the LDS-staged
-// K1 fits 4).  Uniform positions read a VGPR by s_set_gpr_idx + v_readlane;
-// the serial probe chain of snappy_compression.c:384-403 runs in SGPRs with
-// one LDS round trip (the table) per probe.  Output is a token list
-// (pos | len << 16, offset) plus the unit's exact encoded size; K2 writes the
-// bytes once K3 has placed every unit.
+// layout of BASELINE.json configs[1]).
+//
+//  * The unit lives in 140 VGPRs of its wave (v2..v141), "halo" layout:
+//    VGPR r, lane l < 60 holds big-endian dword 60 r + l and lanes 60..63
+//    repeat the next VGPR's first four dwords, so any 4 consecutive dwords
+//    sit in one VGPR: a wave-uniform unaligned load of up to 12 bytes is one
+//    s_set_gpr_idx + v_mov + v_readlanes, with no branches.
+//  * The hash table is u32 in LDS (16 KiB): position (low 16 bits) and a
+//    16-bit tag of the 4 bytes there (high 16 bits).  A probe whose tag
+//    differs is a miss decided without touching the input; equal tags are
+//    verified against the bytes, so the probe/insert sequence of
+//    src/snappy_compression.c:384-403 is reproduced bit for bit.
+//  * Hash and tag of 64 consecutive positions are precomputed lane-parallel
+//    (`hv`, lane l <-> position q0 + l) together with their BE32 (`bv`).
+//  * Each round speculates that the next W probes miss: lane k computes its
+//    probe position in closed form, fetches hash/tag by ds_bpermute and its
+//    table slot by one ds_read; a ballot finds the first tag hit, window
+//    conflict or end.  Earlier lanes are exact misses (inserted in lane
+//    order), the hit is verified against the bytes in registers.
+//  * Output is a token list (pos | len << 16, offset) plus the unit's exact
+//    encoded size; K2 writes the bytes once K3 has placed every unit.
+// VGPR budget <= 168 -> 3 waves per SIMD; LDS 16 KiB -> 10 units per CU.
 // ---------------------------------------------------------------------------
 typedef uint32_t v32 __attribute__((ext_vector_type(32)));
+typedef uint32_t v12u __attribute__((ext_vector_type(12)));
 
-// The unit's 128 VGPRs are four v32 locals g0..g3 of the kernel, pinned to
-// v2..v129 by the asm constraints below so that one s_set_gpr_idx_on +
-// v_mov reads VGPR v[2 + r] for a wave-uniform r (a C++ switch over the four
-// vectors compiles to a branch tree, and passing them by reference or in a
-// struct sends them to scratch).
-#define REG_OF(r)                                                                              \
-    ({                                                                                         \
-        uint32_t _v;                                                                           \
-        asm volatile("s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\tv_mov_b32 %0, v2\n\ts_set_gpr_idx_off" \
-                     : "=&v"(_v)                                                               \
-                     : "s"((uint32_t)(r)), "{v[2:33]}"(g0), "{v[34:65]}"(g1), "{v[66:97]}"(g2),     \
-                       "{v[98:129]}"(g3));                                                     \
-        _v;                                                                                    \
+constexpr uint32_t kTagMul = 0x9E3779B1u;
+constexpr uint32_t kRegs = 140;  // VGPRs holding the unit (60 dwords each): dwords < 8400
+
+// VGPR v[2 + r] of the resident unit (r wave-uniform).  g0..g4 are pinned
+// to v2..v141 by the constraints, so the relative move is exact whatever
+// else the allocator does.
+#define REG_OF(r)                                                                                   \
+    ({                                                                                              \
+        uint32_t _v;                                                                                \
+        asm volatile("s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\tv_mov_b32 %0, v2\n\ts_set_gpr_idx_off"      \
+                     : "=&v"(_v)                                                                    \
+                     : "s"((uint32_t)(r)), "{v[2:33]}"(g0), "{v[34:65]}"(g1), "{v[66:97]}"(g2),          \
+                       "{v[98:129]}"(g3), "{v[130:141]}"(g4));                                      \
+        _v;                                                                                         \
     })
 
-// big-endian dwords d, d+1 of the unit as one u64 (d wave-uniform)
-#define BE_PAIR(dd)                                                                          \
-    ({                                                                                       \
-        const uint32_t _d = (dd);                                                            \
-        const uint32_t _v = REG_OF(_d >> 6);                                                 \
-        const uint32_t _hi = __builtin_amdgcn_readlane(_v, _d & 63);                         \
-        uint32_t _lo;                                                                        \
-        if ((_d & 63) != 63) _lo = __builtin_amdgcn_readlane(_v, (_d & 63) + 1);             \
-        else _lo = _d + 1 < 8192 ? __builtin_amdgcn_readlane(REG_OF((_d >> 6) + 1), 0) : 0; \
-        ((uint64_t)_hi << 32) | _lo;                                                         \
-    })
+// halo layout: dword d -> VGPR d / 60, lane d % 60 (exact for d < 8400)
+#define HALO_R(d) (((d) * 17477u) >> 20)
 
-// BE32 load at byte q (src/snappy_compression.c:239-241)
+// BE32 load at byte q (src/snappy_compression.c:239-241), q wave-uniform
 #define BE32_REG(qq)                                                        \
     ({                                                                      \
         const uint32_t _q = (qq);                                           \
-        (uint32_t)((BE_PAIR(_q >> 2) << (8 * (_q & 3))) >> 32);             \
+        const uint32_t _d = _q >> 2;                                        \
+        const uint32_t _r = HALO_R(_d);                                     \
+        const uint32_t _l = _d - 60 * _r;                                   \
+        const uint32_t _v = REG_OF(_r);                                     \
+        const uint32_t _hi = __builtin_amdgcn_readlane(_v, _l);             \
+        const uint32_t _lo = __builtin_amdgcn_readlane(_v, _l + 1);         \
+        (uint32_t)(((((uint64_t)_hi) << 32 | _lo) << (8 * (_q & 3))) >> 32); \
     })
 
-// 8 bytes at q in memory order (first byte in the top bits)
-#define BE64_REG(qq)                                                        \
-    ({                                                                      \
-        const uint32_t _q8 = (qq);                                          \
-        const uint32_t _s8 = 8 * (_q8 & 3);                                 \
-        const uint64_t _a8 = BE_PAIR(_q8 >> 2);                             \
-        uint64_t _r8 = _a8;                                                 \
-        if (_s8) {                                                          \
-            const uint32_t _c8 = (uint32_t)(BE_PAIR((_q8 >> 2) + 2) >> 32); \
-            _r8 = (_a8 << _s8) | (_c8 >> (32 - _s8));                       \
-        }                                                                   \
-        _r8;                                                                \
-    })
-
-// per-lane BE dword at byte q + 4*lane (q uniform), for wave-parallel compares
-#define BE32_LANES(qq)                                                                               \
-    ({                                                                                               \
-        const uint32_t _ql = (qq);                                                                   \
-        const uint32_t _d0 = _ql >> 2, _r0 = _d0 >> 6;                                              \
-        const uint32_t _v0 = REG_OF(_r0);                                                            \
-        const uint32_t _v1 = _r0 + 1 < 128 ? REG_OF(_r0 + 1) : 0;                                    \
-        const uint32_t _e = (_d0 & 63) + lane, _f = _e + 1;                                          \
-        const uint32_t _a0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_e & 63) << 2), (int)_v0); \
-        const uint32_t _a1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_e & 63) << 2), (int)_v1); \
-        const uint32_t _b0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_f & 63) << 2), (int)_v0); \
-        const uint32_t _b1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_f & 63) << 2), (int)_v1); \
-        const uint32_t _hi = _e < 64 ? _a0 : _a1, _lo = _f < 64 ? _b0 : _b1;                        \
-        const uint32_t _s = 8 * (_ql & 3);                                                           \
-        _s ? (_hi << _s) | (_lo >> (32 - _s)) : _hi;                                                 \
+// per-lane dword e = d0 + lane (d0 uniform): the 64 dwords span at most
+// VGPRs R..R+2 of the halo layout
+#define DW_LANES(dd0)                                                                                  \
+    ({                                                                                                 \
+        const uint32_t _d0 = (dd0);                                                                    \
+        const uint32_t _R = HALO_R(_d0);                                                               \
+        const uint32_t _e = _d0 + lane;                                                                \
+        const uint32_t _re = HALO_R(_e) - _R; /* 0..2 */                                              \
+        const uint32_t _le = _e - 60 * (_R + _re);                                                     \
+        const uint32_t _x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)REG_OF(_R));  \
+        const uint32_t _x1 = (uint32_t)__builtin_amdgcn_ds_bpermute(                                   \
+            (int)(_le << 2), (int)(_R + 1 < kRegs ? REG_OF(_R + 1) : 0));                              \
+        const uint32_t _x2 = (uint32_t)__builtin_amdgcn_ds_bpermute(                                   \
+            (int)(_le << 2), (int)(_R + 2 < kRegs ? REG_OF(_R + 2) : 0));                              \
+        _re == 0 ? _x0 : (_re == 1 ? _x1 : _x2);                                                       \
     })
 
 __device__ __forceinline__ uint32_t varint_len(uint64_t v)
@@ -392,13 +390,102 @@ __device__ __forceinline__ uint32_t copy_bytes(uint32_t len, uint32_t off)
     return 3 * (n64 + has60) + ((last < 12 && off < 2048) ? 2 : 3);
 }
 
+// Window conflicts under the tagged table with lane-ordered inserts (the
+// highest lane of one ds_write wins a shared slot, which is the serial
+// order): lane k must not read a slot an earlier lane writes (h_k in
+// {h_j, a_j}), nor have its a-insert overwritten by an earlier lane's
+// h-insert of another position (a_k == h_j, p_j != p_k - 1).
+// Everything stays in VALU integer ops (a bool in a lane mask would bounce
+// through SGPRs on every compare): eqm(x) = all-ones iff x == 0, for x < 2^31.
+// Lanes with no source lane see 0 (bound_ctrl), which can only add false
+// conflicts; lane 0 is never flagged (the caller masks it), so every round
+// makes progress.
+__device__ __forceinline__ uint32_t eqm(uint32_t x) { return (uint32_t)((int32_t)(x - 1) >> 31); }
+
+template <int N>
+__device__ __forceinline__ uint32_t shz(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x110 + N, 0xF, 0xF, true);
+}
+
+template <int N>
+__device__ __forceinline__ uint32_t tconf_step(uint32_t h, uint32_t a, uint32_t notdup)
+{
+    const uint32_t hs = shz<N>(h), as = shz<N>(a);
+    if constexpr (N == 1) return eqm(h ^ hs) | eqm(h ^ as) | (eqm(a ^ hs) & notdup);
+    else return eqm(h ^ hs) | eqm(h ^ as) | eqm(a ^ hs);
+}
+
+template <int W>
+__device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdup)
+{
+    uint32_t c = 0;
+    if constexpr (W > 1) c |= tconf_step<1>(h, a, notdup);
+    if constexpr (W > 2) c |= tconf_step<2>(h, a, notdup);
+    if constexpr (W > 3) c |= tconf_step<3>(h, a, notdup);
+    if constexpr (W > 4) {
+        c |= tconf_step<4>(h, a, notdup);
+        c |= tconf_step<5>(h, a, notdup);
+        c |= tconf_step<6>(h, a, notdup);
+        c |= tconf_step<7>(h, a, notdup);
+    }
+    if constexpr (W > 8) {
+        c |= tconf_step<8>(h, a, notdup);
+        c |= tconf_step<9>(h, a, notdup);
+        c |= tconf_step<10>(h, a, notdup);
+        c |= tconf_step<11>(h, a, notdup);
+        c |= tconf_step<12>(h, a, notdup);
+        c |= tconf_step<13>(h, a, notdup);
+        c |= tconf_step<14>(h, a, notdup);
+        c |= tconf_step<15>(h, a, notdup);
+    }
+    return c;
+}
+
+// per-lane BE32 at q + 4*lane for lanes 0..15 (q uniform): 17 dwords span
+// at most VGPRs R, R+1 of the halo layout
+#define BE32_LANES16(qq)                                                                             \
+    ({                                                                                               \
+        const uint32_t _q = (qq);                                                                    \
+        const uint32_t _d0 = _q >> 2;                                                                \
+        const uint32_t _R = HALO_R(_d0);                                                             \
+        const uint32_t _e = _d0 + (lane & 15);                                                       \
+        const uint32_t _re = HALO_R(_e) - _R; /* 0..1 */                                            \
+        const uint32_t _le = _e - 60 * (_R + _re);                                                   \
+        const uint32_t _x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)REG_OF(_R));\
+        const uint32_t _x1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_le + 1) << 2), (int)REG_OF(_R));\
+        const uint32_t _y0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)REG_OF(_R + 1));\
+        const uint32_t _y1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_le + 1) << 2), (int)REG_OF(_R + 1));\
+        const uint32_t _hi = _re ? _y0 : _x0, _lo = _re ? _y1 : _x1;                                 \
+        const uint32_t _s = 8 * (_q & 3);                                                            \
+        _s ? (_hi << _s) | (_lo >> (32 - _s)) : _hi;                                                 \
+    })
+
+#ifndef SNAPPY_K1R_WINDOW
+#define SNAPPY_K1R_WINDOW 8
+#endif
+
+#ifdef SNAPPY_K1R_STAMPS
+#define STAMP(var)                                                                          \
+    do {                                                                                    \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory");        \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+    } while (0)
+#define SEG(i, a, b) seg[i] += (b) - (a)
+#else
+#define STAMP(var) do { } while (0)
+#define SEG(i, a, b) do { } while (0)
+#endif
+
 __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
                                                           uint32_t hdr_mode, uint64_t header_value,
                                                           uint2 *__restrict__ tokens, uint32_t tok_cap,
                                                           uint32_t *__restrict__ ntok_out,
                                                           uint32_t *__restrict__ sizes)
 {
-    __shared__ uint16_t table[kTable];
+    constexpr int W = SNAPPY_K1R_WINDOW;
+    __shared__ uint32_t table[kTable];
     const uint32_t lane = threadIdx.x;
     const uint32_t u = blockIdx.x;
     const uint64_t base = (uint64_t)u * unit;
@@ -408,16 +495,18 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
     const uint64_t t_start = clock64();
 #endif
 
-    // unit -> VGPRs, dword d = 64 r + lane, big-endian, zero past the end
+    // unit -> VGPRs (halo layout), big-endian, zero past the end
     v32 g0, g1, g2, g3;
+    v12u g4;
     const bool aligned = ((reinterpret_cast<uintptr_t>(src) & 3) == 0);
 #pragma unroll
-    for (int i = 0; i < 128; i++) {
-        const uint32_t b = 4 * (64 * i + lane);
+    for (int i = 0; i < (int)kRegs; i++) {
+        const uint32_t d = 60 * i + lane;  // lanes 60..63: the next VGPR's first dwords
+        const uint32_t b = 4 * d;
         uint32_t w = 0;
         if (b + 4 <= L && aligned) {
             w = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(src + b));
-        } else {
+        } else if (b < L) {
             for (uint32_t k = 0; k < 4; k++)
                 if (b + k < L) w |= (uint32_t)src[b + k] << (8 * k);
         }
@@ -425,84 +514,169 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
         if (i < 32) g0[i] = w;
         else if (i < 64) g1[i - 32] = w;
         else if (i < 96) g2[i - 64] = w;
-        else g3[i - 96] = w;
+        else if (i < 128) g3[i - 96] = w;
+        else g4[i - 128] = w;
     }
-    for (uint32_t i = lane; i < kTable / 2; i += 64) reinterpret_cast<uint32_t *>(table)[i] = 0;
+
+    uint32_t T = 256, lg = 8;  // set_htable_size :198-204
+    while (T < kTable && T < L) { T <<= 1; lg++; }
+    const uint32_t shift = 32 - lg;
+
+    // never-set slots mean position 0 (snappy_compression.c:259-265): tag of BE32(0)
+    const uint32_t cur0 = BE32_REG(0);
+    const uint32_t init = ((cur0 * kTagMul) >> 16) << 16;
+    for (uint32_t i = lane; i < kTable; i += 64) table[i] = init;
     __syncthreads();
 
     uint32_t enc = 0;
     if (hdr_mode == SNAPPY_HDR_EVERY_UNIT) enc = varint_len(L);
     else if (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0) enc = varint_len(header_value);
 
-    uint32_t T = 256, lg = 8;  // set_htable_size :198-204
-    while (T < kTable && T < L) { T <<= 1; lg++; }
-    const uint32_t shift = 32 - lg;
-
     uint2 *tok = tokens + (uint64_t)u * tok_cap;
     uint32_t tka = 0, tkb = 0;  // 64 pending tokens, lane t holds token t
     uint32_t nt = 0;
 
+    // position window: lane l <-> position q0 + l
+    uint32_t q0 = 0xFFFFFFFFu, hv = 0, bv = 0;
+// lane l <- BE32 at q0 + l (from dwords q0/4 + k, k = ((q0 & 3) + l) / 4 <= 16)
+#define WINDOW_AT(qq)                                                                              \
+    do {                                                                                           \
+        q0 = (qq);                                                                                 \
+        const uint32_t _w = DW_LANES(q0 >> 2);                                                     \
+        const uint32_t _k = ((q0 & 3) + lane) >> 2;                                                \
+        const uint32_t _a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_k << 2), (int)_w);       \
+        const uint32_t _b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_k + 1) << 2), (int)_w); \
+        const uint32_t _s = 8 * ((q0 + lane) & 3);                                                 \
+        bv = _s ? (_a << _s) | (_b >> (32 - _s)) : _a;                                             \
+        hv = ((bv * kMul) >> shift) | (((bv * kTagMul) >> 16) << 16);                              \
+    } while (0)
+
 #ifdef SNAPPY_K1R_STATS
     const uint64_t t_loop = clock64();
-    uint32_t n_probe = 0, n_match = 0;
+    uint32_t n_probe = 0, n_match = 0, n_round = 0;
+    uint64_t t_match = 0;
+#endif
+#ifdef SNAPPY_K1R_STAMPS
+    uint64_t seg[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t s0, s1, s2, s3, s4, s5;
 #endif
     uint32_t p = 1, skip = 33, lit = 0;
     while (!(L - p < (skip >> 5) + 15)) {  // is_block_end :229-232
 #ifdef SNAPPY_K1R_STATS
-        n_probe++;
+        n_round++;
 #endif
-        const uint64_t w = BE_PAIR((p - 1) >> 2) << (8 * ((p - 1) & 3));
-        const uint32_t prev = (uint32_t)(w >> 32);
-        const uint32_t cur = (uint32_t)(w >> 24);
-        const uint32_t h = (cur * kMul) >> shift;
-        const uint32_t cand = __builtin_amdgcn_readfirstlane(table[h]);
-        if (BE32_REG(cand) == cur) {  // found_match :259-265
-            // find_copy_length :61-72: 8 bytes by SALU, then 256 per wave pass
-            uint32_t len = 4;
-            const uint64_t x = BE64_REG(p + 4) ^ BE64_REG(cand + 4);
-            if (x) {
-                len += (uint32_t)__builtin_clzll(x) >> 3;
+        STAMP(s0);
+        if (p - 1 < q0 || p + 12 > q0 + 64) WINDOW_AT(p - 1);
+        STAMP(s1);
+        SEG(0, s0, s1);
+        // ---- speculative window: lane k = k-th probe if all earlier miss
+        const uint32_t sk = skip + lane;
+        const uint32_t pk = p + skipsum(sk) - skipsum(skip);
+        // invalid: lane >= W, block end (is_block_end), or past the window
+        const uint32_t inval = (uint32_t)(((int32_t)(W - 1 - lane)) >> 31) |
+                               (uint32_t)(((int32_t)(L - pk) - (int32_t)((sk >> 5) + 15)) >> 31) |
+                               (uint32_t)(((int32_t)(q0 + 64) - (int32_t)(pk + 12)) >> 31);
+        const uint32_t ik = inval ? 1 : pk - q0;
+        const uint32_t hvp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ik << 2), (int)hv);
+        const uint32_t hvq = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((ik - 1) << 2), (int)hv);
+        const uint32_t h = hvp & 0xFFFF, a = hvq & 0xFFFF;
+        STAMP(s2);
+        SEG(1, s1, s2);
+        const uint32_t ent = table[h];
+        // previous lane stepped by 1 iff its skip counter was 32..63
+        const uint32_t notdup = ~eqm(((sk - 1) >> 5) ^ 1);
+        const uint32_t conflict = tconf<W>(h, a, notdup) & ~eqm(lane);
+        const uint32_t hit = eqm((ent ^ hvp) >> 16);
+        const uint64_t stop = __ballot((inval | conflict | hit) != 0);
+        const uint32_t f = (uint32_t)__builtin_ctzll(stop);
+        STAMP(s3);
+        SEG(2, s2, s3);
+        // lanes before f are exact misses: update_hash_table :303-307
+        if (lane < f) {
+            table[a] = (pk - 1) | (hvq & 0xFFFF0000u);
+            table[h] = pk | (hvp & 0xFFFF0000u);
+        }
+        const uint64_t hits = __ballot((hit & ~(inval | conflict)) != 0);
+        STAMP(s4);
+        SEG(3, s3, s4);
+#ifdef SNAPPY_K1R_STATS
+        n_probe += f + ((hits >> f) & 1);
+#endif
+        uint32_t next_f = f;  // probes consumed if no match
+        if ((hits >> f) & 1) {
+#ifdef SNAPPY_K1R_STATS
+            const uint64_t tm0 = clock64();
+#endif
+            const uint32_t pf = __builtin_amdgcn_readlane(pk, f);
+            const uint32_t cand = __builtin_amdgcn_readlane(ent, f) & 0xFFFF;
+            const uint32_t hf = __builtin_amdgcn_readlane(hvp, f);
+            // lanes 0..15 compare BE32 at pf + 4j and cand + 4j: verification
+            // (first 4 bytes) and find_copy_length :61-72 up to 64 bytes at once
+            const uint32_t y = (BE32_LANES16(pf) ^ BE32_LANES16(cand)) & (uint32_t)(((int32_t)(lane - 16)) >> 31);
+            const uint64_t bad = __ballot(y != 0);
+            uint32_t len;
+            if (bad) {
+                const uint32_t m = (uint32_t)__builtin_ctzll(bad);
+                len = 4 * m + ((uint32_t)__builtin_clz(__builtin_amdgcn_readlane(y, m)) >> 3);
             } else {
-                len = 12;
+                len = 64;  // 252 bytes per wave pass from here
                 for (;;) {
-                    if (p + len >= L) break;
-                    const uint32_t y = BE32_LANES(p + len) ^ BE32_LANES(cand + len);
-                    const uint64_t bad = __ballot(y != 0);
-                    if (bad) {
-                        const uint32_t m = (uint32_t)__builtin_ctzll(bad);
-                        const uint32_t ym = __builtin_amdgcn_readlane(y, m);
-                        len += 4 * m + ((uint32_t)__builtin_clz(ym) >> 3);
+                    if (pf + len >= L) break;
+                    const uint32_t qa = pf + len, qb = cand + len;
+                    const uint32_t a0 = DW_LANES(qa >> 2), b0 = DW_LANES(qb >> 2);
+                    const int nx = (int)(((lane + 1) & 63) << 2);
+                    const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute(nx, (int)a0);
+                    const uint32_t b1 = (uint32_t)__builtin_amdgcn_ds_bpermute(nx, (int)b0);
+                    const uint32_t sa = 8 * (qa & 3), sb = 8 * (qb & 3);
+                    const uint32_t va = sa ? (a0 << sa) | (a1 >> (32 - sa)) : a0;
+                    const uint32_t vb = sb ? (b0 << sb) | (b1 >> (32 - sb)) : b0;
+                    const uint32_t yy = lane < 63 ? (va ^ vb) : 0;  // lane 63 lacks its successor
+                    const uint64_t bb = __ballot(yy != 0);
+                    if (bb) {
+                        const uint32_t m = (uint32_t)__builtin_ctzll(bb);
+                        len += 4 * m + ((uint32_t)__builtin_clz(__builtin_amdgcn_readlane(yy, m)) >> 3);
                         break;
                     }
-                    len += 256;
+                    len += 252;
                 }
             }
-            if (len > L - p) len = L - p;  // the compare never runs past the block
+            if (len >= 4) {  // verified: found_match :259-265
+                if (len > L - pf) len = L - pf;  // the compare never runs past the block
 #ifdef SNAPPY_K1R_STATS
-            n_match++;
+                n_match++;
 #endif
-            const uint32_t off = p - cand;
-            if (p > lit) enc += literal_bytes(p - lit);
-            enc += copy_bytes(len, off);
-            if (lane == (nt & 63)) {
-                tka = p | (len << 16);
-                tkb = off;
+                const uint32_t off = pf - cand;
+                if (pf > lit) enc += literal_bytes(pf - lit);
+                enc += copy_bytes(len, off);
+                if (lane == (nt & 63)) {
+                    tka = pf | (len << 16);
+                    tkb = off;
+                }
+                nt++;
+                if ((nt & 63) == 0) tok[nt - 64 + lane] = make_uint2(tka, tkb);
+                table[hf & 0xFFFF] = pf | (hf & 0xFFFF0000u);  // emit_copy :328
+                skip = 32;
+                p = pf + len;
+                lit = p;
+#ifdef SNAPPY_K1R_STATS
+                t_match += clock64() - tm0;
+#endif
+                continue;
             }
-            nt++;
-            if ((nt & 63) == 0) tok[nt - 64 + lane] = make_uint2(tka, tkb);
-            if (lane == 0) table[h] = (uint16_t)p;  // emit_copy :328
-            skip = 32;
-            p += len;
-            lit = p;
-        } else {  // update_hash_table :303-307, append_literal :283-287
-            if (lane == 0) {
-                table[(prev * kMul) >> shift] = (uint16_t)(p - 1);
-                table[h] = (uint16_t)p;
-            }
-            p += skip >> 5;
-            skip++;
+            // tag collision: lane f is a miss as well
+            const uint32_t af = __builtin_amdgcn_readlane(hvq, f);
+            table[af & 0xFFFF] = (pf - 1) | (af & 0xFFFF0000u);
+            table[hf & 0xFFFF] = pf | (hf & 0xFFFF0000u);
+            next_f = f + 1;
         }
+        // f (or f + 1) misses consumed; f stops at a conflict, the window
+        // edge or the block end and is retried exactly as the next lane 0
+        p = p + skipsum(skip + next_f) - skipsum(skip);
+        skip += next_f;
+        STAMP(s5);
+        SEG(4, s4, s5);
     }
+#undef WINDOW_AT
     if (L > lit) enc += literal_bytes(L - lit);
     if (lane < (nt & 63)) tok[(nt & ~63u) + lane] = make_uint2(tka, tkb);
     if (lane == 0) {
@@ -511,12 +685,18 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
     }
 #ifdef SNAPPY_K1R_STATS
     if (lane == 0) {
-        // debug side channel: 4 u64 per unit after the token area of unit 0..
         uint64_t *st = reinterpret_cast<uint64_t *>(tokens + (uint64_t)gridDim.x * tok_cap) + 4 * (uint64_t)u;
         st[0] = clock64() - t_loop;
-        st[1] = t_loop - t_start;
-        st[2] = n_probe;
+#ifdef SNAPPY_K1R_STAMPS
+        t_match = seg[0] | (seg[1] << 16 << 16);
+        st[3] = seg[2] | (seg[3] << 32);
+        st[2] = seg[4];
+#endif
+        st[1] = t_match;
+#ifndef SNAPPY_K1R_STAMPS
+        st[2] = n_probe | ((uint64_t)n_round << 32);
         st[3] = n_match;
+#endif
     }
 #endif
 }

@@ -7,7 +7,8 @@ os.environ["SNAPPY_AMD_LIB"] = os.path.join(ROOT, "lightweight-snappy_amd", "var
 import numpy as np, torch
 import datagen, snappy_amd
 kind = sys.argv[1] if len(sys.argv) > 1 else "T"
-n, chunk = 256 << 20, 32768
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 256 << 20
+chunk = 32768
 a = datagen.make(kind, n, 1234 if kind == "T" else 1)
 x = torch.from_numpy(a).cuda()
 c = snappy_amd.Codec(0)
@@ -27,6 +28,8 @@ hip = ctypes.CDLL("libamdhip64.so")
 buf = np.empty(units * 4, dtype=np.uint64)
 rc = hip.hipMemcpy(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ctx.tokens + units * tok_cap * 8), ctypes.c_size_t(buf.nbytes), 2)
 st = buf.reshape(units, 4)
-loop, start, probes, matches = st[:, 0], st[:, 1], st[:, 2], st[:, 3]
-print(f"{kind}: units {units} probes/unit {probes.mean():.0f} matches/unit {matches.mean():.0f}")
-print(f"loop cycles/unit {loop.mean():.0f}  start cycles/unit {start.mean():.0f}  cycles/probe {loop.sum() / probes.sum():.1f}")
+loop, tmatch, pr, matches = st[:, 0], st[:, 1], st[:, 2], st[:, 3]
+probes, rounds = pr & 0xFFFFFFFF, pr >> 32
+print(f"{kind}: units {units} probes/unit {probes.mean():.0f} rounds/unit {rounds.mean():.0f} matches/unit {matches.mean():.0f}")
+print(f"loop cycles/unit {loop.mean():.0f} cycles/probe {loop.sum() / probes.sum():.1f} cycles/round {loop.sum()/rounds.sum():.1f}"
+      f" match-path cycles/match {tmatch.sum()/max(matches.sum(),1):.1f} non-match cycles/round {(loop.sum()-tmatch.sum())/rounds.sum():.1f}")

@@ -854,24 +854,41 @@ __global__ __launch_bounds__(256) void k3_gather(const uint8_t *__restrict__ scr
 }
 
 // ---------------------------------------------------------------------------
-// K4: one wave per unit.  LDS: [decoded window: unit bytes][compressed unit].
-// Tag dispatch of src/snappy_decompression.c:290-333 with bounds checks; a
-// copy whose source lies before the unit start is an error here (the
-// reference compressor never emits one; K5 detects them in foreign streams).
+// K4: one wave per unit; LDS holds only the decoded window (unit bytes), so
+// 32 KiB units run 5 per CU.  The compressed unit streams through a 512-byte
+// register window (cur = bytes [B, B+256), nxt = [B+256, B+512), one dword
+// per lane, nxt prefetched a window ahead); tags are parsed in SALU from
+// v_readlane, elements are executed lane-parallel into LDS: literals from the
+// window by ds_bpermute (long ones straight from HBM), copies as one LDS read
+// + write per <= 64 bytes with the byte-serial overlap semantics of
+// src/snappy_decompression.c:273-280 (out[op+j] = out[op-off + j mod off]).
+// Tag dispatch of :290-333 with bounds checks; a copy reaching before the
+// unit start is an error here (the reference compressor never emits one).
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t load_dw_guarded(const uint8_t *comp, uint64_t a, uint64_t lim)
+{
+    // dword at 4-aligned absolute address a; bytes at or past lim read as 0
+    if (a + 4 <= lim) return __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(comp + a));
+    uint32_t w = 0;
+    for (uint32_t k = 0; k < 4; k++)
+        if (a + k < lim) w |= (uint32_t)comp[a + k] << (8 * k);
+    return w;
+}
+
+#ifdef SNAPPY_K4_STATS
+__device__ uint64_t g_k4_stats[32768 * 4];
+#endif
+
 __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restrict__ comp,
                                                           const uint64_t *__restrict__ offsets, uint64_t n,
                                                           uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
-                                                          uint32_t comp_cap,
-                                                          uint8_t *__restrict__ out, int32_t *__restrict__ status)
+                                                          uint32_t comp_cap, uint8_t *__restrict__ out,
+                                                          int32_t *__restrict__ status)
 {
     extern __shared__ uint32_t lds[];
+    uint8_t *ob = reinterpret_cast<uint8_t *>(lds);
     const uint32_t lane = threadIdx.x;
     const uint32_t u = blockIdx.x;
-    const uint32_t win = (unit + 15) & ~15u;
-    uint8_t *ob = reinterpret_cast<uint8_t *>(lds);
-    uint32_t *cw = lds + win / 4 + 4;
-
     const uint64_t c0 = offsets[u], c1 = offsets[u + 1];
     const uint64_t base = (uint64_t)u * unit;
     const uint32_t want = (uint32_t)((n - base) < unit ? (n - base) : unit);
@@ -882,33 +899,24 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
     }
     const uint32_t clen = (uint32_t)(c1 - c0);
 
-    // Stage compressed bytes: aligned dwords covering [c0 & ~3, c1); the
-    // unit's byte i then sits at cb[mis + i].
-    const uint32_t mis = (uint32_t)(c0 & 3);
-    const uint64_t a0 = c0 - mis;
-    const uint32_t span = clen + mis;
-    const uint32_t nfull = span >> 2;
-    const uint32_t *gw = reinterpret_cast<const uint32_t *>(comp + a0);
-    for (uint32_t k = lane; k < nfull; k += 64) cw[k] = __builtin_nontemporal_load(gw + k);
-    if (lane == 0) {
-        uint32_t w = 0;
-        for (uint32_t i = nfull * 4; i < span; i++) w |= (uint32_t)comp[a0 + i] << (8 * (i - nfull * 4));
-        cw[nfull] = w;
-        cw[nfull + 1] = 0;
-        cw[nfull + 2] = 0;
-    }
-    __syncthreads();
-    const uint8_t *cb = reinterpret_cast<const uint8_t *>(cw) + mis;
+    // register window over the compressed unit (absolute 4-aligned base B)
+    uint64_t B = c0 & ~3ull;
+    uint32_t cur = load_dw_guarded(comp, B + 4 * lane, c1);
+    uint32_t nxt = load_dw_guarded(comp, B + 256 + 4 * lane, c1);
+    // dword k (0..127) of [cur | nxt], k uniform
+#define WDW(k) ((uint32_t)((k) < 64 ? __builtin_amdgcn_readlane(cur, (k)) : __builtin_amdgcn_readlane(nxt, (k) - 64)))
 
-    uint32_t ip = 0, op = 0;
+    uint32_t ip = 0, op = 0;  // ip relative to c0
     // varint preamble: every STREAMS unit, and block 0 of a SINGLE stream
     if (hdr_mode == SNAPPY_HDR_EVERY_UNIT || (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0)) {
         const uint64_t expect = hdr_mode == SNAPPY_HDR_EVERY_UNIT ? want : header_value;
+        const uint32_t o = (uint32_t)(c0 - B);
         uint64_t v = 0;
         uint32_t k = 0;
         bool done = false;
         for (; k < 10 && k < clen; k++) {
-            const uint32_t byte = rfl(le32_at(cw, mis + k) & 0xFF);
+            const uint32_t q = o + k;
+            const uint32_t byte = (WDW(q >> 2) >> (8 * (q & 3))) & 0xFF;
             v |= (uint64_t)(byte & 0x7F) << (7 * k);
             if (!(byte & 0x80)) { done = true; k++; break; }
         }
@@ -916,53 +924,119 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
         ip = k;
     }
 
+#ifdef SNAPPY_K4_STATS
+    const uint64_t t_loop = clock64();
+    uint32_t n_el = 0, n_lit = 0;
+#endif
     while (st == SNAPPY_ST_OK && op < want) {
+#ifdef SNAPPY_K4_STATS
+        n_el++;
+#endif
         if (ip >= clen) { st = SNAPPY_ST_TRUNCATED; break; }
-        const uint32_t w = rfl(le32_at(cw, mis + ip));
-        const uint32_t tag = w & 0xFF;
+        uint32_t o = (uint32_t)(c0 + ip - B);
+        if (o >= 256) {
+            if (o < 512) {  // slide the window by 256 bytes, prefetch the next one
+                B += 256;
+                cur = nxt;
+                o -= 256;
+            } else {  // jumped past the window (long literal): restart it here
+                B = (c0 + ip) & ~3ull;
+                cur = load_dw_guarded(comp, B + 4 * lane, c1);
+                o = (uint32_t)(c0 + ip - B);
+            }
+            nxt = load_dw_guarded(comp, B + 256 + 4 * lane, c1);
+        }
+        // tag + 4 following bytes: dwords o/4 .. o/4+1 (o < 256 -> indices < 66)
+        const uint32_t d = o >> 2;
+        const uint64_t w = ((uint64_t)WDW(d + 1) << 32) | WDW(d);
+        const uint32_t x0 = (uint32_t)(w >> (8 * (o & 3)));        // tag, b1, b2, b3
+        const uint32_t x1 = (uint32_t)(((uint64_t)WDW(d + 2) << 32 | WDW(d + 1)) >> (8 * (o & 3)));  // b4..b7
+        const uint32_t tag = x0 & 0xFF;
         uint32_t len, off;
         if ((tag & 3) == 0) {
             len = (tag >> 2) + 1;
-            ip += 1;
+            uint32_t hl = 1;
             if (len > 60) {
                 const uint32_t k = len - 60;
-                if (ip + k > clen) { st = SNAPPY_ST_TRUNCATED; break; }
-                const uint32_t x = rfl(le32_at(cw, mis + ip));
-                len = (k == 4 ? x : (x & ((1u << (8 * k)) - 1))) + 1;
-                ip += k;
+                hl = 1 + k;
+                if (ip + hl > clen) { st = SNAPPY_ST_TRUNCATED; break; }
+                const uint32_t v = k == 4 ? ((x0 >> 8) | (x1 << 24)) : ((x0 >> 8) & ((1u << (8 * k)) - 1));
+                len = v + 1;
             }
-            if (len > clen - ip) { st = SNAPPY_ST_TRUNCATED; break; }
+            if (len > clen - ip - hl) { st = SNAPPY_ST_TRUNCATED; break; }
             if (len > want - op) { st = SNAPPY_ST_OVERRUN; break; }
-            for (uint32_t b = lane; b < len; b += 64) ob[op + b] = cb[ip + b];
-            ip += len;
+            const uint32_t s0 = o + hl;  // literal start within [cur | nxt]
+            if (s0 + len <= 508) {
+                // <= 64 bytes per pass from the register window
+                for (uint32_t b = 0; b < len; b += 64) {
+                    const uint32_t q = s0 + b + lane;
+                    const uint32_t dd = q >> 2;
+                    const uint32_t va = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((dd & 63) << 2), (int)cur);
+                    const uint32_t vb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((dd & 63) << 2), (int)nxt);
+                    const uint32_t v = dd < 64 ? va : vb;
+                    if (b + lane < len) ob[op + b + lane] = (uint8_t)(v >> (8 * (q & 3)));
+                }
+            } else {
+                // long literal: straight from HBM, 256 bytes per pass
+                const uint8_t *lsrc = comp + c0 + ip + hl;
+                for (uint32_t b = 0; b < len; b += 256) {
+                    uint8_t v[4];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const uint32_t j = b + 64 * k + lane;
+                        v[k] = j < len ? lsrc[j] : 0;
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const uint32_t j = b + 64 * k + lane;
+                        if (j < len) ob[op + j] = v[k];
+                    }
+                }
+            }
+            ip += hl + len;
             op += len;
+#ifdef SNAPPY_K4_STATS
+            n_lit++;
+#endif
             continue;
         }
         if ((tag & 3) == 1) {
             len = ((tag >> 2) & 7) + 4;
-            off = ((tag >> 5) << 8) | ((w >> 8) & 0xFF);
+            off = ((tag >> 5) << 8) | ((x0 >> 8) & 0xFF);
             ip += 2;
         } else if ((tag & 3) == 2) {
             len = (tag >> 2) + 1;
-            off = (w >> 8) & 0xFFFF;
+            off = (x0 >> 8) & 0xFFFF;
             ip += 3;
         } else {
             len = (tag >> 2) + 1;
-            off = rfl(le32_at(cw, mis + ip + 1));
+            off = (x0 >> 8) | (x1 << 24);
             ip += 5;
         }
         if (ip > clen) { st = SNAPPY_ST_TRUNCATED; break; }
         if (off == 0 || off > op) { st = SNAPPY_ST_OFFSET; break; }
         if (len > want - op) { st = SNAPPY_ST_OVERRUN; break; }
-        // byte-serial overlap semantics (snappy_decompression.c:273-280):
-        // out[op+i] = out[op-off + i mod off]
+        // out[op+j] = out[op-off + j mod off]; j mod off via a float reciprocal
+        // (exact for j < 64)
         if (lane < len) {
-            const uint32_t i = off >= len ? lane : lane % off;
-            const uint8_t v = ob[op - off + i];
-            ob[op + lane] = v;
+            uint32_t j = lane;
+            if (off < len) {
+                const float r = __builtin_amdgcn_rcpf((float)off);
+                const uint32_t qd = (uint32_t)((float)lane * r + 0.0001f);
+                j = lane - qd * off;
+            }
+            ob[op + lane] = ob[op - off + j];
         }
         op += len;
     }
+#undef WDW
+#ifdef SNAPPY_K4_STATS
+    if (lane == 0 && u < 32768) {
+        g_k4_stats[4 * u] = clock64() - t_loop;
+        g_k4_stats[4 * u + 1] = n_el;
+        g_k4_stats[4 * u + 2] = n_lit;
+    }
+#endif
     __syncthreads();
 
     // write the window out (unit-aligned destination)
@@ -1083,3 +1157,11 @@ __global__ __launch_bounds__(64) void k5_index_stream(const uint8_t *__restrict_
 }
 
 }  // namespace snappy_amd
+
+#ifdef SNAPPY_K4_STATS
+extern "C" int snappy_amd_debug_k4_stats(uint64_t *host, size_t count)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(snappy_amd::g_k4_stats), count * sizeof(uint64_t), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -7;
+}
+#endif

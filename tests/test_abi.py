@@ -74,3 +74,14 @@ def test_no_oracle_in_product():
                 assert "liboracle" not in src and "import oracle" not in src, f
     out = subprocess.run(["ldd", snappy_amd.LIB_PATH], capture_output=True, text=True).stdout
     assert "oracle" not in out and "snappy_ref" not in out
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/src"), reason="reference sources only in the build container")
+def test_reference_cli_links_against_library(tmp_path):
+    # the reference's own src/cmd.c, unchanged, links against libsnappy_amd.so
+    src = "/root/reference/src"
+    exe = tmp_path / "snappy_dropin"
+    r = subprocess.run(["gcc", "-O2", "-w", "-I", INC, "-o", str(exe), f"{src}/cmd.c", f"{src}/IO_utils.c",
+                        f"{src}/result.c", "-L", os.path.dirname(snappy_amd.LIB_PATH), "-lsnappy_amd"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

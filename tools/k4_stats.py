@@ -1,0 +1,23 @@
+#!/usr/bin/env python3
+"""Cycles per element of K4 (SNAPPY_K4_STATS build)."""
+import ctypes, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "lightweight-snappy_amd"))
+os.environ["SNAPPY_AMD_LIB"] = os.path.join(ROOT, "lightweight-snappy_amd", "variants", "libsnappy_amd_k4stats.so")
+import numpy as np, torch
+import datagen, snappy_amd
+kind = sys.argv[1]; n = int(sys.argv[2]); chunk = 32768
+a = datagen.make(kind, n, 1234 if kind == "T" else 1)
+x = torch.from_numpy(a).cuda()
+c = snappy_amd.Codec(0)
+comp, offs = c.compress_tensor(x, chunk=chunk, layout=snappy_amd.STREAMS)
+back = c.decompress_tensor(comp, offs, n, chunk=chunk, layout=snappy_amd.STREAMS)
+assert torch.equal(back, x)
+units = n // chunk
+buf = np.zeros(units * 4, dtype=np.uint64)
+lib = snappy_amd.lib()
+lib.snappy_amd_debug_k4_stats.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+assert lib.snappy_amd_debug_k4_stats(buf.ctypes.data_as(ctypes.c_void_p), units * 4) == 0
+st = buf.reshape(units, 4)
+print(f"{kind} units {units}: elements/unit {st[:,1].mean():.0f} literals/unit {st[:,2].mean():.0f} "
+      f"cycles/unit {st[:,0].mean():.0f} cycles/element {st[:,0].sum()/st[:,1].sum():.1f}")

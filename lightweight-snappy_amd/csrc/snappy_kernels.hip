@@ -928,10 +928,12 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
     const uint64_t t_loop = clock64();
     uint32_t n_el = 0, n_lit = 0;
 #endif
+    // [cur | nxt] byte-window gathers (q per lane, < 512)
+#define WIN_DW(qd) ({ const uint32_t _qd = (qd);                                                     \
+        const uint32_t _a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_qd & 63) << 2), (int)cur);   \
+        const uint32_t _b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_qd & 63) << 2), (int)nxt);   \
+        _qd < 64 ? _a : _b; })
     while (st == SNAPPY_ST_OK && op < want) {
-#ifdef SNAPPY_K4_STATS
-        n_el++;
-#endif
         if (ip >= clen) { st = SNAPPY_ST_TRUNCATED; break; }
         uint32_t o = (uint32_t)(c0 + ip - B);
         if (o >= 256) {
@@ -946,89 +948,139 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
             }
             nxt = load_dw_guarded(comp, B + 256 + 4 * lane, c1);
         }
-        // tag + 4 following bytes: dwords o/4 .. o/4+1 (o < 256 -> indices < 66)
-        const uint32_t d = o >> 2;
-        const uint64_t w = ((uint64_t)WDW(d + 1) << 32) | WDW(d);
-        const uint32_t x0 = (uint32_t)(w >> (8 * (o & 3)));        // tag, b1, b2, b3
-        const uint32_t x1 = (uint32_t)(((uint64_t)WDW(d + 2) << 32 | WDW(d + 1)) >> (8 * (o & 3)));  // b4..b7
+        // ---- lane-parallel candidate parse: an element starting at o + lane
+        const uint32_t q = o + lane;  // < 320
+        const uint32_t dA = WIN_DW(q >> 2), dB = WIN_DW((q >> 2) + 1);
+        const uint32_t sh = 8 * (q & 3);
+        const uint32_t x0 = sh ? (dA >> sh) | (dB << (32 - sh)) : dA;  // tag, t1, t2, t3
+        const uint32_t dC = WIN_DW((q >> 2) + 2);
+        const uint32_t x1 = sh ? (dB >> sh) | (dC << (32 - sh)) : dB;  // t4..t7
         const uint32_t tag = x0 & 0xFF;
-        uint32_t len, off;
-        if ((tag & 3) == 0) {
-            len = (tag >> 2) + 1;
-            uint32_t hl = 1;
-            if (len > 60) {
-                const uint32_t k = len - 60;
-                hl = 1 + k;
-                if (ip + hl > clen) { st = SNAPPY_ST_TRUNCATED; break; }
-                const uint32_t v = k == 4 ? ((x0 >> 8) | (x1 << 24)) : ((x0 >> 8) & ((1u << (8 * k)) - 1));
-                len = v + 1;
-            }
-            if (len > clen - ip - hl) { st = SNAPPY_ST_TRUNCATED; break; }
-            if (len > want - op) { st = SNAPPY_ST_OVERRUN; break; }
-            const uint32_t s0 = o + hl;  // literal start within [cur | nxt]
-            if (s0 + len <= 508) {
-                // <= 64 bytes per pass from the register window
-                for (uint32_t b = 0; b < len; b += 64) {
-                    const uint32_t q = s0 + b + lane;
-                    const uint32_t dd = q >> 2;
-                    const uint32_t va = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((dd & 63) << 2), (int)cur);
-                    const uint32_t vb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((dd & 63) << 2), (int)nxt);
-                    const uint32_t v = dd < 64 ? va : vb;
-                    if (b + lane < len) ob[op + b + lane] = (uint8_t)(v >> (8 * (q & 3)));
+        uint32_t size, olen, info;  // info: copy offset, or literal header length
+        const uint32_t t = tag & 3;
+        if (t == 0) {
+            const uint32_t m = tag >> 2;
+            const uint32_t k = m >= 60 ? m - 59 : 0;  // extra length bytes
+            const uint32_t v = k == 0 ? m : (k == 4 ? ((x0 >> 8) | (x1 << 24)) : ((x0 >> 8) & ((1u << (8 * k)) - 1)));
+            olen = v + 1;  // may be huge for garbage candidates: clamped by the checks below
+            info = 1 + k;
+            size = info + olen;
+        } else if (t == 1) {
+            olen = ((tag >> 2) & 7) + 4;
+            info = ((tag >> 5) << 8) | ((x0 >> 8) & 0xFF);
+            size = 2;
+        } else if (t == 2) {
+            olen = (tag >> 2) + 1;
+            info = (x0 >> 8) & 0xFFFF;
+            size = 3;
+        } else {
+            olen = (tag >> 2) + 1;
+            info = (x0 >> 8) | (x1 << 24);
+            size = 5;
+        }
+        // ---- element chain from lane 0 by pointer doubling: J^k(0) for lane k
+        uint32_t nx = lane + (size < 64 ? size : 64);  // >= 64: leaves the window
+#define JUMP(T, idx) ({ const uint32_t _i = (idx);                                                   \
+        const uint32_t _g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_i & 63) << 2), (int)(T));    \
+        _i < 64 ? _g : _i; })
+        const uint32_t J1 = nx;
+        const uint32_t J2 = JUMP(J1, J1);
+        const uint32_t J4 = JUMP(J2, J2);
+        const uint32_t J8 = JUMP(J4, J4);
+        const uint32_t J16 = JUMP(J8, J8);
+        const uint32_t J32 = JUMP(J16, J16);
+        // (bpermute must run with every lane active: select afterwards)
+        uint32_t pos = 0;
+        { const uint32_t g = JUMP(J1, pos); pos = (lane & 1) ? g : pos; }
+        { const uint32_t g = JUMP(J2, pos); pos = (lane & 2) ? g : pos; }
+        { const uint32_t g = JUMP(J4, pos); pos = (lane & 4) ? g : pos; }
+        { const uint32_t g = JUMP(J8, pos); pos = (lane & 8) ? g : pos; }
+        { const uint32_t g = JUMP(J16, pos); pos = (lane & 16) ? g : pos; }
+        { const uint32_t g = JUMP(J32, pos); pos = (lane & 32) ? g : pos; }
+#undef JUMP
+        // lane k < E holds element k of the batch (starts are increasing)
+        const uint64_t inwin = __ballot(pos < 64);
+        uint32_t E = (uint32_t)__builtin_popcountll(inwin);
+        const uint32_t pg = pos < 64 ? pos : 0;
+        const uint32_t e_t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pg << 2), (int)t);
+        const uint32_t e_size = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pg << 2), (int)size);
+        const uint32_t e_len = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pg << 2), (int)olen);
+        const uint32_t e_info = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pg << 2), (int)info);
+        // exclusive prefix sums of compressed sizes and output lengths over
+        // the batch (64-bit safe: garbage past E is zeroed)
+        const bool live = lane < E;
+        uint32_t tot_in, tot_out;
+        const uint32_t in_off = wave_excl_scan(live ? e_size : 0, lane, &tot_in);
+        const uint32_t out_off = wave_excl_scan(live ? e_len : 0, lane, &tot_out);
+        // validity in stream order: stop at the first element that runs past the
+        // unit (truncated / overrun), reaches before the unit start, or past want
+        const uint32_t e_ip = ip + in_off, e_op = op + out_off;
+        int32_t e_err = SNAPPY_ST_OK;
+        if (e_op >= want) e_err = 1;  // done before this element: not an error
+        else if (e_size > clen - e_ip) e_err = SNAPPY_ST_TRUNCATED;
+        else if (e_len > want - e_op) e_err = SNAPPY_ST_OVERRUN;
+        else if (e_t != 0 && (e_info == 0 || e_info > e_op)) e_err = SNAPPY_ST_OFFSET;
+        const uint64_t badm = __ballot(live && e_err != SNAPPY_ST_OK);
+        uint32_t nexec = E;
+        if (badm) {
+            nexec = (uint32_t)__builtin_ctzll(badm);
+            const int32_t er = __builtin_amdgcn_readlane(e_err, nexec);
+            if (er != 1) st = er;
+        }
+        // ---- execute elements 0..nexec-1 in order (lane-parallel bytes)
+        for (uint32_t k = 0; k < nexec; k++) {
+            const uint32_t kt = __builtin_amdgcn_readlane(e_t, k);
+            const uint32_t kl = __builtin_amdgcn_readlane(e_len, k);
+            const uint32_t ki = __builtin_amdgcn_readlane(e_info, k);
+            const uint32_t kop = __builtin_amdgcn_readlane(e_op, k);
+            if (kt != 0) {
+                if (lane < kl) {
+                    uint32_t j = lane;
+                    if (ki < kl) {
+                        const float r = __builtin_amdgcn_rcpf((float)ki);
+                        const uint32_t qd = (uint32_t)((float)lane * r + 0.0001f);
+                        j = lane - qd * ki;
+                    }
+                    ob[kop + lane] = ob[kop - ki + j];
                 }
             } else {
-                // long literal: straight from HBM, 256 bytes per pass
-                const uint8_t *lsrc = comp + c0 + ip + hl;
-                for (uint32_t b = 0; b < len; b += 256) {
-                    uint8_t v[4];
-#pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        const uint32_t j = b + 64 * k + lane;
-                        v[k] = j < len ? lsrc[j] : 0;
+                const uint32_t kip = __builtin_amdgcn_readlane(e_ip, k);
+                const uint32_t s0 = (uint32_t)(c0 + kip - B) + ki;  // literal start in [cur | nxt]
+                if (s0 + kl <= 508) {
+                    for (uint32_t b = 0; b < kl; b += 64) {
+                        const uint32_t qq = s0 + b + lane;
+                        const uint32_t v = WIN_DW(qq >> 2);
+                        if (b + lane < kl) ob[kop + b + lane] = (uint8_t)(v >> (8 * (qq & 3)));
                     }
+                } else {
+                    const uint8_t *lsrc = comp + c0 + kip + ki;
+                    for (uint32_t b = 0; b < kl; b += 256) {
+                        uint8_t v[4];
 #pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        const uint32_t j = b + 64 * k + lane;
-                        if (j < len) ob[op + j] = v[k];
+                        for (int m = 0; m < 4; m++) {
+                            const uint32_t jj = b + 64 * m + lane;
+                            v[m] = jj < kl ? lsrc[jj] : 0;
+                        }
+#pragma unroll
+                        for (int m = 0; m < 4; m++) {
+                            const uint32_t jj = b + 64 * m + lane;
+                            if (jj < kl) ob[kop + jj] = v[m];
+                        }
                     }
                 }
             }
-            ip += hl + len;
-            op += len;
+        }
 #ifdef SNAPPY_K4_STATS
-            n_lit++;
+        n_el += nexec;
 #endif
-            continue;
+        if (nexec) {
+            ip += __builtin_amdgcn_readlane(in_off, nexec - 1) + __builtin_amdgcn_readlane(e_size, nexec - 1);
+            op += __builtin_amdgcn_readlane(out_off, nexec - 1) + __builtin_amdgcn_readlane(e_len, nexec - 1);
+        } else if (st == SNAPPY_ST_OK && op < want) {
+            st = SNAPPY_ST_TRUNCATED;  // no progress possible
         }
-        if ((tag & 3) == 1) {
-            len = ((tag >> 2) & 7) + 4;
-            off = ((tag >> 5) << 8) | ((x0 >> 8) & 0xFF);
-            ip += 2;
-        } else if ((tag & 3) == 2) {
-            len = (tag >> 2) + 1;
-            off = (x0 >> 8) & 0xFFFF;
-            ip += 3;
-        } else {
-            len = (tag >> 2) + 1;
-            off = (x0 >> 8) | (x1 << 24);
-            ip += 5;
-        }
-        if (ip > clen) { st = SNAPPY_ST_TRUNCATED; break; }
-        if (off == 0 || off > op) { st = SNAPPY_ST_OFFSET; break; }
-        if (len > want - op) { st = SNAPPY_ST_OVERRUN; break; }
-        // out[op+j] = out[op-off + j mod off]; j mod off via a float reciprocal
-        // (exact for j < 64)
-        if (lane < len) {
-            uint32_t j = lane;
-            if (off < len) {
-                const float r = __builtin_amdgcn_rcpf((float)off);
-                const uint32_t qd = (uint32_t)((float)lane * r + 0.0001f);
-                j = lane - qd * off;
-            }
-            ob[op + lane] = ob[op - off + j];
-        }
-        op += len;
     }
+#undef WIN_DW
 #undef WDW
 #ifdef SNAPPY_K4_STATS
     if (lane == 0 && u < 32768) {

@@ -190,6 +190,8 @@ static int compress_impl(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t
                            c->ntok, c->sizes);
         HIP_OK(hipGetLastError());
         if (c->timing) (void)hipEventRecord(c->ev[1], c->stream);
+        hipLaunchKernelGGL(k2s_size_units, dim3((uint32_t)units), dim3(64), 0, c->stream, (uint64_t)n, unit, hm,
+                           header_value, c->tokens, tok_cap, c->ntok, c->sizes);
         hipLaunchKernelGGL(k3_scan, dim3(1), dim3(1024), 0, c->stream, c->sizes, (uint64_t)units, d_offsets, c->total);
         hipLaunchKernelGGL(k2_emit_units, dim3((uint32_t)units), dim3(64), 0, c->stream,
                            static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens, tok_cap,

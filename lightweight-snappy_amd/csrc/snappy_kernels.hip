@@ -23,6 +23,10 @@
 
 namespace snappy_amd {
 
+// v_writelane_b32 (no clang builtin in this toolchain): the LLVM intrinsic by name
+__device__ int amdgcn_writelane(int val, int lanesel, int old) __asm("llvm.amdgcn.writelane.i32");
+
+
 constexpr uint32_t kTable = 4096;
 constexpr uint32_t kMul = 0x1e35a7bdu;
 
@@ -465,13 +469,18 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
 #define SNAPPY_K1R_WINDOW 8
 #endif
 
-#ifdef SNAPPY_K1R_STAMPS
-#define STAMP(var)                                                                          \
+#if defined(SNAPPY_K1R_STAMPS) || defined(SNAPPY_K1R_MSTAMPS)
+#define MSTAMP(var)                                                                         \
     do {                                                                                    \
         __builtin_amdgcn_sched_barrier(0);                                                  \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory");        \
         __builtin_amdgcn_sched_barrier(0);                                                  \
     } while (0)
+#else
+#define MSTAMP(var) do { } while (0)
+#endif
+#ifdef SNAPPY_K1R_STAMPS
+#define STAMP(var) MSTAMP(var)
 #define SEG(i, a, b) seg[i] += (b) - (a)
 #else
 #define STAMP(var) do { } while (0)
@@ -528,21 +537,19 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
     for (uint32_t i = lane; i < kTable; i += 64) table[i] = init;
     __syncthreads();
 
-    uint32_t enc = 0;
-    if (hdr_mode == SNAPPY_HDR_EVERY_UNIT) enc = varint_len(L);
-    else if (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0) enc = varint_len(header_value);
-
     uint2 *tok = tokens + (uint64_t)u * tok_cap;
     uint32_t tka = 0, tkb = 0;  // 64 pending tokens, lane t holds token t
     uint32_t nt = 0;
 
     // position window: lane l <-> position q0 + l
-    uint32_t q0 = 0xFFFFFFFFu, hv = 0, bv = 0;
-// lane l <- BE32 at q0 + l (from dwords q0/4 + k, k = ((q0 & 3) + l) / 4 <= 16)
+    uint32_t q0 = 0xFFFFFFFFu, hv = 0, bv = 0, dv = 0;
+// lane l <- BE32 at q0 + l (from dwords q0/4 + k, k = ((q0 & 3) + l) / 4 <= 16);
+// dv keeps the dwords q0/4 + l themselves (the match side of a verification)
 #define WINDOW_AT(qq)                                                                              \
     do {                                                                                           \
         q0 = (qq);                                                                                 \
-        const uint32_t _w = DW_LANES(q0 >> 2);                                                     \
+        dv = DW_LANES(q0 >> 2);                                                                    \
+        const uint32_t _w = dv;                                                                    \
         const uint32_t _k = ((q0 & 3) + lane) >> 2;                                                \
         const uint32_t _a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_k << 2), (int)_w);       \
         const uint32_t _b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_k + 1) << 2), (int)_w); \
@@ -556,7 +563,7 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
     uint32_t n_probe = 0, n_match = 0, n_round = 0;
     uint64_t t_match = 0;
 #endif
-#ifdef SNAPPY_K1R_STAMPS
+#if defined(SNAPPY_K1R_STAMPS) || defined(SNAPPY_K1R_MSTAMPS)
     uint64_t seg[6] = {0, 0, 0, 0, 0, 0};
     uint64_t s0, s1, s2, s3, s4, s5;
 #endif
@@ -607,13 +614,27 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
 #ifdef SNAPPY_K1R_STATS
             const uint64_t tm0 = clock64();
 #endif
+#ifdef SNAPPY_K1R_MSTAMPS
+            uint64_t m0, m1, m2, m3;
+            MSTAMP(m0);
+#endif
             const uint32_t pf = __builtin_amdgcn_readlane(pk, f);
             const uint32_t cand = __builtin_amdgcn_readlane(ent, f) & 0xFFFF;
             const uint32_t hf = __builtin_amdgcn_readlane(hvp, f);
             // lanes 0..15 compare BE32 at pf + 4j and cand + 4j: verification
             // (first 4 bytes) and find_copy_length :61-72 up to 64 bytes at once
-            const uint32_t y = (BE32_LANES16(pf) ^ BE32_LANES16(cand)) & (uint32_t)(((int32_t)(lane - 16)) >> 31);
+            // pf side from the dword window (pf <= q0 + 52, so dword index <= 30)
+            const uint32_t kp = (pf >> 2) - (q0 >> 2) + (lane & 15);
+            const uint32_t pa = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(kp << 2), (int)dv);
+            const uint32_t pb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((kp + 1) << 2), (int)dv);
+            const uint32_t ps = 8 * (pf & 3);
+            const uint32_t pv = ps ? (pa << ps) | (pb >> (32 - ps)) : pa;
+            const uint32_t y = (pv ^ BE32_LANES16(cand)) & (uint32_t)(((int32_t)(lane - 16)) >> 31);
             const uint64_t bad = __ballot(y != 0);
+#ifdef SNAPPY_K1R_MSTAMPS
+            MSTAMP(m1);
+            seg[0] += m1 - m0;
+#endif
             uint32_t len;
             if (bad) {
                 const uint32_t m = (uint32_t)__builtin_ctzll(bad);
@@ -640,24 +661,29 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
                     len += 252;
                 }
             }
+#ifdef SNAPPY_K1R_MSTAMPS
+            MSTAMP(m2);
+            seg[1] += m2 - m1;
+#endif
             if (len >= 4) {  // verified: found_match :259-265
                 if (len > L - pf) len = L - pf;  // the compare never runs past the block
 #ifdef SNAPPY_K1R_STATS
                 n_match++;
 #endif
                 const uint32_t off = pf - cand;
-                if (pf > lit) enc += literal_bytes(pf - lit);
-                enc += copy_bytes(len, off);
-                if (lane == (nt & 63)) {
-                    tka = pf | (len << 16);
-                    tkb = off;
-                }
+                // token t goes to lane t & 63 of (tka, tkb)
+                tka = (uint32_t)amdgcn_writelane((int)(pf | (len << 16)), (int)(nt & 63), (int)tka);
+                tkb = (uint32_t)amdgcn_writelane((int)off, (int)(nt & 63), (int)tkb);
                 nt++;
                 if ((nt & 63) == 0) tok[nt - 64 + lane] = make_uint2(tka, tkb);
                 table[hf & 0xFFFF] = pf | (hf & 0xFFFF0000u);  // emit_copy :328
                 skip = 32;
                 p = pf + len;
                 lit = p;
+#ifdef SNAPPY_K1R_MSTAMPS
+                MSTAMP(m3);
+                seg[2] += m3 - m2;
+#endif
 #ifdef SNAPPY_K1R_STATS
                 t_match += clock64() - tm0;
 #endif
@@ -677,23 +703,21 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
         SEG(4, s4, s5);
     }
 #undef WINDOW_AT
-    if (L > lit) enc += literal_bytes(L - lit);
+    (void)lit;
+    (void)sizes;
     if (lane < (nt & 63)) tok[(nt & ~63u) + lane] = make_uint2(tka, tkb);
-    if (lane == 0) {
-        ntok_out[u] = nt;
-        sizes[u] = enc;
-    }
+    if (lane == 0) ntok_out[u] = nt;
 #ifdef SNAPPY_K1R_STATS
     if (lane == 0) {
         uint64_t *st = reinterpret_cast<uint64_t *>(tokens + (uint64_t)gridDim.x * tok_cap) + 4 * (uint64_t)u;
         st[0] = clock64() - t_loop;
-#ifdef SNAPPY_K1R_STAMPS
+#if defined(SNAPPY_K1R_STAMPS) || defined(SNAPPY_K1R_MSTAMPS)
         t_match = seg[0] | (seg[1] << 16 << 16);
         st[3] = seg[2] | (seg[3] << 32);
         st[2] = seg[4];
 #endif
         st[1] = t_match;
-#ifndef SNAPPY_K1R_STAMPS
+#if !defined(SNAPPY_K1R_STAMPS) && !defined(SNAPPY_K1R_MSTAMPS)
         st[2] = n_probe | ((uint64_t)n_round << 32);
         st[3] = n_match;
 #endif
@@ -718,6 +742,49 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
     }
     *total = (uint32_t)__shfl((int)x, 63, 64);
     return x - v;
+}
+
+// K2s: exact encoded size of every unit from its token list (header +
+// literal headers/bytes + copy pieces), one wave per unit, one token per lane.
+__global__ __launch_bounds__(64) void k2s_size_units(uint64_t n, uint32_t unit, uint32_t hdr_mode,
+                                                     uint64_t header_value, const uint2 *__restrict__ tokens,
+                                                     uint32_t tok_cap, const uint32_t *__restrict__ ntok,
+                                                     uint32_t *__restrict__ sizes)
+{
+    const uint32_t lane = threadIdx.x;
+    const uint32_t u = blockIdx.x;
+    const uint64_t base = (uint64_t)u * unit;
+    const uint32_t L = (uint32_t)((n - base) < unit ? (n - base) : unit);
+    uint32_t enc = 0;
+    if (hdr_mode == SNAPPY_HDR_EVERY_UNIT) enc = varint_len(L);
+    else if (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0) enc = varint_len(header_value);
+    const uint2 *tok = tokens + (uint64_t)u * tok_cap;
+    const uint32_t nt = ntok[u];
+    uint32_t carry = 0, acc = 0;
+    for (uint32_t c = 0; c <= nt; c += 64) {
+        const uint32_t t = c + lane;
+        uint32_t pos = L, len = 0, off = 0;
+        if (t < nt) {
+            const uint2 k = tok[t];
+            pos = k.x & 0xFFFF;
+            len = k.x >> 16;
+            off = k.y;
+        }
+        const uint32_t end = pos + len;
+        uint32_t prev_end = (uint32_t)__shfl_up((int)end, 1, 64);
+        if (lane == 0) prev_end = carry;
+        uint32_t b = 0;
+        if (t <= nt) {
+            const uint32_t litn = pos - prev_end;
+            b = (litn ? literal_bytes(litn) : 0) + (len ? copy_bytes(len, off) : 0);
+        }
+        acc += b;
+        carry = (uint32_t)__shfl((int)end, 63, 64);
+    }
+    // wave sum
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) acc += (uint32_t)__shfl_xor((int)acc, d, 64);
+    if (lane == 0) sizes[u] = enc + acc;
 }
 
 __device__ __forceinline__ void put_copy(uint8_t *o, uint32_t len, uint32_t off)

@@ -3,7 +3,7 @@
 import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "lightweight-snappy_amd"))
-os.environ["SNAPPY_AMD_LIB"] = os.path.join(ROOT, "lightweight-snappy_amd", "variants", "libsnappy_amd_stamps.so")
+os.environ["SNAPPY_AMD_LIB"] = os.path.join(ROOT, "lightweight-snappy_amd", "variants", "libsnappy_amd_" + (sys.argv[3] if len(sys.argv) > 3 else "stamps") + ".so")
 import numpy as np, torch
 import datagen, snappy_amd
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 8 << 20
@@ -29,7 +29,7 @@ seg0, seg1 = (st[:, 1] & 0xFFFFFFFF).astype(float), (st[:, 1] >> 32).astype(floa
 seg2, seg3 = (st[:, 3] & 0xFFFFFFFF).astype(float), (st[:, 3] >> 32).astype(float)
 seg4 = st[:, 2].astype(float)
 rounds = 4333
-names = ["window", "lanes+bpermute", "table+conflict+ballot", "inserts+ballot2", "match/advance"]
+names = sys.argv[2].split(",") if len(sys.argv) > 2 else ["window", "lanes+bpermute", "table+conflict+ballot", "inserts+ballot2", "match/advance"]
 tot = loop.sum()
 for nm, v in zip(names, [seg0, seg1, seg2, seg3, seg4]):
     print(f"{nm:24s} {v.sum()/tot*100:5.1f}%  {v.mean()/rounds:7.1f} cycles/round")

@@ -456,10 +456,11 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
         const uint32_t _e = _d0 + (lane & 15);                                                       \
         const uint32_t _re = HALO_R(_e) - _R; /* 0..1 */                                            \
         const uint32_t _le = _e - 60 * (_R + _re);                                                   \
-        const uint32_t _x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)REG_OF(_R));\
-        const uint32_t _x1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_le + 1) << 2), (int)REG_OF(_R));\
-        const uint32_t _y0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)REG_OF(_R + 1));\
-        const uint32_t _y1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_le + 1) << 2), (int)REG_OF(_R + 1));\
+        const uint32_t _r0 = REG_OF(_R), _r1 = REG_OF(_R + 1);                                      \
+        const uint32_t _x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)_r0);      \
+        const uint32_t _x1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_le + 1) << 2), (int)_r0);\
+        const uint32_t _y0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)_r1);      \
+        const uint32_t _y1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_le + 1) << 2), (int)_r1);\
         const uint32_t _hi = _re ? _y0 : _x0, _lo = _re ? _y1 : _x1;                                 \
         const uint32_t _s = 8 * (_q & 3);                                                            \
         _s ? (_hi << _s) | (_lo >> (32 - _s)) : _hi;                                                 \
@@ -567,7 +568,7 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
     uint64_t seg[6] = {0, 0, 0, 0, 0, 0};
     uint64_t s0, s1, s2, s3, s4, s5;
 #endif
-    uint32_t p = 1, skip = 33, lit = 0;
+    uint32_t p = 1, skip = 33;
     while (!(L - p < (skip >> 5) + 15)) {  // is_block_end :229-232
 #ifdef SNAPPY_K1R_STATS
         n_round++;
@@ -679,7 +680,6 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
                 table[hf & 0xFFFF] = pf | (hf & 0xFFFF0000u);  // emit_copy :328
                 skip = 32;
                 p = pf + len;
-                lit = p;
 #ifdef SNAPPY_K1R_MSTAMPS
                 MSTAMP(m3);
                 seg[2] += m3 - m2;
@@ -703,7 +703,6 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
         SEG(4, s4, s5);
     }
 #undef WINDOW_AT
-    (void)lit;
     (void)sizes;
     if (lane < (nt & 63)) tok[(nt & ~63u) + lane] = make_uint2(tka, tkb);
     if (lane == 0) ntok_out[u] = nt;
@@ -732,16 +731,43 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
 // them out (src/snappy_compression.c:95-165).  The last pseudo-token carries
 // the tail literal.
 // ---------------------------------------------------------------------------
+// Wave-wide inclusive add-scan in DPP (row_shr 1/2/4/8 inside 16-lane rows,
+// then row_bcast:15 / row_bcast:31 across rows): no LDS round trips.
+template <uint32_t CTRL, uint32_t ROWS>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, true);
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
+{
+    x += dpp0<0x111, 0xF>(x);
+    x += dpp0<0x112, 0xF>(x);
+    x += dpp0<0x114, 0xF>(x);
+    x += dpp0<0x118, 0xF>(x);
+    x += dpp0<0x142, 0xA>(x);
+    x += dpp0<0x143, 0xC>(x);
+    return x;
+}
+
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, uint32_t *total)
 {
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-        if (lane >= (uint32_t)d) x += y;
-    }
-    *total = (uint32_t)__shfl((int)x, 63, 64);
+    (void)lane;
+    const uint32_t x = wave_incl_scan(v);
+    *total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
     return x - v;
+}
+
+// wave-wide OR, uniform result
+__device__ __forceinline__ uint32_t wave_or(uint32_t x)
+{
+    x |= dpp0<0x111, 0xF>(x);
+    x |= dpp0<0x112, 0xF>(x);
+    x |= dpp0<0x114, 0xF>(x);
+    x |= dpp0<0x118, 0xF>(x);
+    x |= dpp0<0x142, 0xA>(x);
+    x |= dpp0<0x143, 0xC>(x);
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
 // K2s: exact encoded size of every unit from its token list (header +
@@ -1094,46 +1120,79 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
             const int32_t er = __builtin_amdgcn_readlane(e_err, nexec);
             if (er != 1) st = er;
         }
-        // ---- execute elements 0..nexec-1 in order (lane-parallel bytes)
-        for (uint32_t k = 0; k < nexec; k++) {
-            const uint32_t kt = __builtin_amdgcn_readlane(e_t, k);
-            const uint32_t kl = __builtin_amdgcn_readlane(e_len, k);
-            const uint32_t ki = __builtin_amdgcn_readlane(e_info, k);
-            const uint32_t kop = __builtin_amdgcn_readlane(e_op, k);
-            if (kt != 0) {
-                if (lane < kl) {
-                    uint32_t j = lane;
-                    if (ki < kl) {
-                        const float r = __builtin_amdgcn_rcpf((float)ki);
-                        const uint32_t qd = (uint32_t)((float)lane * r + 0.0001f);
-                        j = lane - qd * ki;
+        // ---- a literal whose bytes leave the register window ends the batch;
+        // as the batch's first element it is copied straight from HBM
+        const uint32_t e_lsrc = (uint32_t)(c0 + e_ip - B) + e_info;  // literal data, window byte offset
+        const uint64_t longm = __ballot(lane < nexec && e_t == 0 && e_lsrc + e_len > 508);
+        if (longm) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(longm);
+            if (k == 0) {
+                nexec = 1;
+                const uint32_t kl = __builtin_amdgcn_readlane(e_len, 0);
+                const uint32_t kop = __builtin_amdgcn_readlane(e_op, 0);
+                const uint32_t kip = __builtin_amdgcn_readlane(e_ip, 0);
+                const uint32_t ki = __builtin_amdgcn_readlane(e_info, 0);
+                const uint8_t *lsrc = comp + c0 + kip + ki;
+                for (uint32_t b = 0; b < kl; b += 256) {
+                    uint8_t v[4];
+#pragma unroll
+                    for (int m = 0; m < 4; m++) {
+                        const uint32_t jj = b + 64 * m + lane;
+                        v[m] = jj < kl ? lsrc[jj] : 0;
                     }
-                    ob[kop + lane] = ob[kop - ki + j];
+#pragma unroll
+                    for (int m = 0; m < 4; m++) {
+                        const uint32_t jj = b + 64 * m + lane;
+                        if (jj < kl) ob[kop + jj] = v[m];
+                    }
                 }
             } else {
-                const uint32_t kip = __builtin_amdgcn_readlane(e_ip, k);
-                const uint32_t s0 = (uint32_t)(c0 + kip - B) + ki;  // literal start in [cur | nxt]
-                if (s0 + kl <= 508) {
-                    for (uint32_t b = 0; b < kl; b += 64) {
-                        const uint32_t qq = s0 + b + lane;
-                        const uint32_t v = WIN_DW(qq >> 2);
-                        if (b + lane < kl) ob[kop + b + lane] = (uint8_t)(v >> (8 * (qq & 3)));
-                    }
-                } else {
-                    const uint8_t *lsrc = comp + c0 + kip + ki;
-                    for (uint32_t b = 0; b < kl; b += 256) {
-                        uint8_t v[4];
-#pragma unroll
-                        for (int m = 0; m < 4; m++) {
-                            const uint32_t jj = b + 64 * m + lane;
-                            v[m] = jj < kl ? lsrc[jj] : 0;
-                        }
-#pragma unroll
-                        for (int m = 0; m < 4; m++) {
-                            const uint32_t jj = b + 64 * m + lane;
-                            if (jj < kl) ob[kop + jj] = v[m];
-                        }
-                    }
+                nexec = k;
+            }
+        }
+        // ---- byte passes over the batch output [op, op_end), 64 bytes each:
+        // byte lane l finds its element from the bitmap of element starts in
+        // the pass, literals read the register window, copies read LDS.  A
+        // copy byte whose source lies in the same pass waits for the sub-pass
+        // that wrote it (out[op+j] = out[op-off + j mod off], :273-280).
+        if (nexec && !(longm && (longm & 1))) {
+            const uint32_t op_end = op + __builtin_amdgcn_readlane(out_off, nexec - 1) +
+                                    __builtin_amdgcn_readlane(e_len, nexec - 1);
+            const bool ex = lane < nexec;
+            const uint32_t kop = e_op | (e_t == 0 ? 0x80000000u : 0u);
+            const uint32_t kinfo = e_t == 0 ? e_lsrc : e_info;
+            const uint32_t mlo = lane >= 31 ? 0xFFFFFFFFu : (2u << lane) - 1;
+            const uint32_t mhi = lane < 32 ? 0u : (lane == 63 ? 0xFFFFFFFFu : (2u << (lane - 32)) - 1);
+            for (uint32_t P = op; P < op_end; P += 64) {
+                const uint32_t j = e_op - P;
+                const bool inw = ex && j < 64;
+                const uint32_t slo = wave_or(inw && j < 32 ? 1u << (j & 31) : 0u);
+                const uint32_t shi = wave_or(inw && j >= 32 ? 1u << (j & 31) : 0u);
+                const uint32_t cb = (uint32_t)__builtin_popcountll(__ballot(ex && e_op < P));
+                const uint32_t id = cb + __builtin_popcount(slo & mlo) + __builtin_popcount(shi & mhi) - 1;
+                const uint32_t f_op = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((id & 63) << 2), (int)kop);
+                const uint32_t f_in = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((id & 63) << 2), (int)kinfo);
+                const uint32_t o = P + lane;
+                const bool lit = (f_op >> 31) != 0;
+                uint32_t d = o - (f_op & 0x7FFFFFFFu);
+                // literal byte from the window (computed by every lane: bpermute needs them all)
+                const uint32_t q = (f_in + d) & 511;
+                const uint32_t lw = WIN_DW(q >> 2);
+                const uint8_t lb = (uint8_t)(lw >> (8 * (q & 3)));
+                if (!lit && d >= f_in && f_in) {  // overlapping copy (off < len <= 64)
+                    const float r = __builtin_amdgcn_rcpf((float)f_in);
+                    const uint32_t qd = (uint32_t)((float)d * r + 0.0001f);
+                    d -= qd * f_in;
+                }
+                const uint32_t src = (f_op & 0x7FFFFFFFu) - f_in + d;
+                bool pend = o < op_end;
+                uint64_t written = 0;
+                for (;;) {
+                    const bool rdy = pend && (lit || src < P || ((written >> ((src - P) & 63)) & 1));
+                    if (rdy) ob[o] = lit ? lb : ob[src];
+                    written |= __ballot(rdy);
+                    pend = pend && !rdy;
+                    if (!__ballot(pend)) break;
                 }
             }
         }

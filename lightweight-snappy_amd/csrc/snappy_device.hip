@@ -58,7 +58,22 @@ static int grow(void **ptr, size_t *cap, size_t need)
 }
 
 static size_t k1_lds_bytes(uint32_t unit) { return 8192 + ((unit + 15) & ~15u); }
-static size_t k4_lds_bytes(uint32_t unit, uint32_t comp_cap) { (void)comp_cap; return ((unit + 15) & ~15u); }
+// K4 output ring: the whole unit when it fits 8 KiB, else an 8 KiB ring
+// (20 units per CU; SNAPPY_AMD_K4_RING overrides, power of two >= 4 KiB)
+static uint32_t k4_ring_bytes(uint32_t unit)
+{
+    static uint32_t cap = 0;
+    if (!cap) {
+        cap = 8192;
+        if (const char *e = getenv("SNAPPY_AMD_K4_RING")) {
+            const unsigned long v = strtoul(e, nullptr, 10);
+            if (v >= 4096 && v <= 65536 && (v & (v - 1)) == 0) cap = (uint32_t)v;
+        }
+    }
+    uint32_t r = 1024;
+    while (r < unit && r < cap) r <<= 1;
+    return r;
+}
 
 extern "C" {
 
@@ -262,9 +277,10 @@ static int decompress_launch(snappy_amd_ctx *c, const void *d_comp, const uint64
     // decoder rejects (TRUNCATED) anything larger than this LDS window.
     const uint32_t comp_cap = (uint32_t)(((uint64_t)unit + unit / 32 + 64 + 15) & ~15ull);
     if (c->timing) (void)hipEventRecord(c->ev[3], c->stream);
-    hipLaunchKernelGGL(k4_decompress_units, dim3((uint32_t)units), dim3(64), k4_lds_bytes(unit, comp_cap), c->stream,
+    const uint32_t ring = k4_ring_bytes(unit);
+    hipLaunchKernelGGL(k4_decompress_units, dim3((uint32_t)units), dim3(64), ring, c->stream,
                        static_cast<const uint8_t *>(d_comp), d_offsets, (uint64_t)n, unit, hdr_mode_of(layout, flags),
-                       header_value, comp_cap,
+                       header_value, comp_cap, ring,
                        static_cast<uint8_t *>(d_out), c->status);
     HIP_OK(hipGetLastError());
     if (c->timing) (void)hipEventRecord(c->ev[4], c->stream);

@@ -53,7 +53,7 @@ __global__ void k3_gather(const uint8_t *__restrict__ scratch, uint64_t stride, 
                           const uint64_t *__restrict__ offsets, uint8_t *__restrict__ out);
 __global__ void k4_decompress_units(const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets,
                                     uint64_t n, uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
-                                    uint32_t comp_cap,
+                                    uint32_t comp_cap, uint32_t ring,
                                     uint8_t *__restrict__ out, int32_t *__restrict__ status);
 __global__ void k5_index_stream(const uint8_t *__restrict__ comp, uint64_t clen, uint64_t *__restrict__ offsets,
                                 uint64_t max_units, int64_t *__restrict__ result);

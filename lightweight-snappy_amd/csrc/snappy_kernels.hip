@@ -968,18 +968,47 @@ __device__ __forceinline__ uint32_t load_dw_guarded(const uint8_t *comp, uint64_
     return w;
 }
 
+// ring -> HBM for output bytes [F, T): 16-byte stores on a 16-aligned
+// destination, bytes otherwise
+__device__ __forceinline__ void k4_flush(const uint8_t *ob, uint32_t M, uint8_t *dst, uint32_t F, uint32_t T,
+                                         uint32_t lane)
+{
+    if (T <= F) return;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        uint32_t a = (F + 15) & ~15u;
+        if (a > T) a = T;
+        if (F + lane < a) dst[F + lane] = ob[(F + lane) & M];
+        const uint32_t e = T & ~15u;
+        for (uint32_t x = a + 16 * lane; x < e; x += 1024)
+            *reinterpret_cast<u32x4 *>(dst + x) = *reinterpret_cast<const u32x4 *>(ob + (x & M));
+        const uint32_t t0 = e > a ? e : a;
+        if (t0 + lane < T) dst[t0 + lane] = ob[(t0 + lane) & M];
+    } else {
+        for (uint32_t x = F + lane; x < T; x += 64) dst[x] = ob[x & M];
+    }
+}
+
 #ifdef SNAPPY_K4_STATS
-__device__ uint64_t g_k4_stats[32768 * 4];
+__device__ uint64_t g_k4_stats[32768 * 8];
+#define K4STAMP(var)                                                                        \
+    do {                                                                                    \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory");        \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+    } while (0)
+#else
+#define K4STAMP(var) do { } while (0)
 #endif
 
 __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restrict__ comp,
                                                           const uint64_t *__restrict__ offsets, uint64_t n,
                                                           uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
-                                                          uint32_t comp_cap, uint8_t *__restrict__ out,
+                                                          uint32_t comp_cap, uint32_t ring, uint8_t *__restrict__ out,
                                                           int32_t *__restrict__ status)
 {
     extern __shared__ uint32_t lds[];
-    uint8_t *ob = reinterpret_cast<uint8_t *>(lds);
+    uint8_t *ob = reinterpret_cast<uint8_t *>(lds);  // output ring: position x -> ob[x & M]
+    const uint32_t M = ring - 1;
     const uint32_t lane = threadIdx.x;
     const uint32_t u = blockIdx.x;
     const uint64_t c0 = offsets[u], c1 = offsets[u + 1];
@@ -991,6 +1020,8 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
         return;
     }
     const uint32_t clen = (uint32_t)(c1 - c0);
+    uint8_t *dst = out + base;
+    uint32_t F = 0;  // output bytes [0, F) are in HBM; [F, op) only in the ring
 
     // register window over the compressed unit (absolute 4-aligned base B)
     uint64_t B = c0 & ~3ull;
@@ -1019,7 +1050,8 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
 
 #ifdef SNAPPY_K4_STATS
     const uint64_t t_loop = clock64();
-    uint32_t n_el = 0, n_lit = 0;
+    uint32_t n_el = 0, n_batch = 0, n_pass = 0, n_sub = 0;
+    uint64_t sg0 = 0, sg1 = 0, sg2 = 0, ta, tb, tc, td;
 #endif
     // [cur | nxt] byte-window gathers (q per lane, < 512)
 #define WIN_DW(qd) ({ const uint32_t _qd = (qd);                                                     \
@@ -1028,6 +1060,7 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
         _qd < 64 ? _a : _b; })
     while (st == SNAPPY_ST_OK && op < want) {
         if (ip >= clen) { st = SNAPPY_ST_TRUNCATED; break; }
+        K4STAMP(ta);
         uint32_t o = (uint32_t)(c0 + ip - B);
         if (o >= 256) {
             if (o < 512) {  // slide the window by 256 bytes, prefetch the next one
@@ -1071,6 +1104,7 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
             info = (x0 >> 8) | (x1 << 24);
             size = 5;
         }
+        K4STAMP(tb);
         // ---- element chain from lane 0 by pointer doubling: J^k(0) for lane k
         uint32_t nx = lane + (size < 64 ? size : 64);  // >= 64: leaves the window
 #define JUMP(T, idx) ({ const uint32_t _i = (idx);                                                   \
@@ -1120,6 +1154,7 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
             const int32_t er = __builtin_amdgcn_readlane(e_err, nexec);
             if (er != 1) st = er;
         }
+        K4STAMP(tc);
         // ---- a literal whose bytes leave the register window ends the batch;
         // as the batch's first element it is copied straight from HBM
         const uint32_t e_lsrc = (uint32_t)(c0 + e_ip - B) + e_info;  // literal data, window byte offset
@@ -1133,6 +1168,9 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
                 const uint32_t kip = __builtin_amdgcn_readlane(e_ip, 0);
                 const uint32_t ki = __builtin_amdgcn_readlane(e_info, 0);
                 const uint8_t *lsrc = comp + c0 + kip + ki;
+                // everything before the literal goes out first; the literal is
+                // written to HBM and to the ring (later copies read its tail)
+                k4_flush(ob, M, dst, F, kop, lane);
                 for (uint32_t b = 0; b < kl; b += 256) {
                     uint8_t v[4];
 #pragma unroll
@@ -1143,9 +1181,13 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
 #pragma unroll
                     for (int m = 0; m < 4; m++) {
                         const uint32_t jj = b + 64 * m + lane;
-                        if (jj < kl) ob[kop + jj] = v[m];
+                        if (jj < kl) {
+                            ob[(kop + jj) & M] = v[m];
+                            dst[kop + jj] = v[m];
+                        }
                     }
                 }
+                F = kop + kl;
             } else {
                 nexec = k;
             }
@@ -1156,8 +1198,14 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
         // copy byte whose source lies in the same pass waits for the sub-pass
         // that wrote it (out[op+j] = out[op-off + j mod off], :273-280).
         if (nexec && !(longm && (longm & 1))) {
+            // the ring must hold [F, op_end): cut the batch (never below one element)
+            const uint64_t over = __ballot(ring < want && lane < nexec && lane > 0 &&
+                                           op + out_off + e_len - F > ring - 64);
+            if (over) nexec = (uint32_t)__builtin_ctzll(over);
             const uint32_t op_end = op + __builtin_amdgcn_readlane(out_off, nexec - 1) +
                                     __builtin_amdgcn_readlane(e_len, nexec - 1);
+            // ring slots below lo were overwritten (or are being): read those from HBM
+            const uint32_t lo = op_end > ring ? op_end - ring : 0;
             const bool ex = lane < nexec;
             const uint32_t kop = e_op | (e_t == 0 ? 0x80000000u : 0u);
             const uint32_t kinfo = e_t == 0 ? e_lsrc : e_info;
@@ -1189,19 +1237,41 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
                 uint64_t written = 0;
                 for (;;) {
                     const bool rdy = pend && (lit || src < P || ((written >> ((src - P) & 63)) & 1));
-                    if (rdy) ob[o] = lit ? lb : ob[src];
+                    if (rdy) {
+                        uint8_t v = lb;
+                        if (!lit) v = src >= lo ? ob[src & M] : dst[src];
+                        ob[o & M] = v;
+                    }
                     written |= __ballot(rdy);
                     pend = pend && !rdy;
+#ifdef SNAPPY_K4_STATS
+                    n_sub++;
+#endif
                     if (!__ballot(pend)) break;
                 }
+#ifdef SNAPPY_K4_STATS
+                n_pass++;
+#endif
             }
         }
+        K4STAMP(td);
+#ifdef SNAPPY_K4_STATS
+        sg0 += tb - ta;
+        sg1 += tc - tb;
+        sg2 += td - tc;
+        n_batch++;
+#endif
 #ifdef SNAPPY_K4_STATS
         n_el += nexec;
 #endif
         if (nexec) {
             ip += __builtin_amdgcn_readlane(in_off, nexec - 1) + __builtin_amdgcn_readlane(e_size, nexec - 1);
             op += __builtin_amdgcn_readlane(out_off, nexec - 1) + __builtin_amdgcn_readlane(e_len, nexec - 1);
+            if (op - F >= 2048) {
+                const uint32_t T = op & ~1023u;
+                k4_flush(ob, M, dst, F, T, lane);
+                F = T;
+            }
         } else if (st == SNAPPY_ST_OK && op < want) {
             st = SNAPPY_ST_TRUNCATED;  // no progress possible
         }
@@ -1210,29 +1280,20 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
 #undef WDW
 #ifdef SNAPPY_K4_STATS
     if (lane == 0 && u < 32768) {
-        g_k4_stats[4 * u] = clock64() - t_loop;
-        g_k4_stats[4 * u + 1] = n_el;
-        g_k4_stats[4 * u + 2] = n_lit;
+        uint64_t *g = g_k4_stats + 8 * u;
+        g[0] = clock64() - t_loop;
+        g[1] = n_el;
+        g[2] = n_batch;
+        g[3] = n_pass;
+        g[4] = n_sub;
+        g[5] = sg0;
+        g[6] = sg1;
+        g[7] = sg2;
     }
 #endif
     __syncthreads();
 
-    // write the window out (unit-aligned destination)
-    uint8_t *dst = out + base;
-    if (((reinterpret_cast<uintptr_t>(dst) | want) & 15) == 0) {
-        for (uint32_t i = lane * 16; i < want; i += 1024)
-            *reinterpret_cast<u32x4 *>(dst + i) = *reinterpret_cast<const u32x4 *>(ob + i);
-    } else {
-        const uint32_t mis2 = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 3);
-        uint32_t head = (4 - mis2) & 3;
-        if (head > want) head = want;
-        if (lane < head) dst[lane] = ob[lane];
-        const uint32_t nw = (want - head) >> 2;
-        uint32_t *dw = reinterpret_cast<uint32_t *>(dst + head);
-        for (uint32_t k = lane; k < nw; k += 64) dw[k] = le32_at(lds, head + 4 * k);
-        const uint32_t t0 = head + 4 * nw;
-        if (lane < want - t0) dst[t0 + lane] = ob[t0 + lane];
-    }
+    k4_flush(ob, M, dst, F, op < want ? op : want, lane);
     if (lane == 0) status[u] = st;
 }
 

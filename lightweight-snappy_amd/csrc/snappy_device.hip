@@ -58,13 +58,15 @@ static int grow(void **ptr, size_t *cap, size_t need)
 }
 
 static size_t k1_lds_bytes(uint32_t unit) { return 8192 + ((unit + 15) & ~15u); }
-// K4 output ring: the whole unit when it fits 8 KiB, else an 8 KiB ring
-// (20 units per CU; SNAPPY_AMD_K4_RING overrides, power of two >= 4 KiB)
+// K4 output ring: the whole unit when it fits 4 KiB, else a 4 KiB ring (the
+// wave-slot limit, 28 units per CU at 85 SGPRs, binds before LDS does; copies
+// reaching further back read HBM).  SNAPPY_AMD_K4_RING overrides (power of
+// two >= 4 KiB).
 static uint32_t k4_ring_bytes(uint32_t unit)
 {
     static uint32_t cap = 0;
     if (!cap) {
-        cap = 8192;
+        cap = 4096;
         if (const char *e = getenv("SNAPPY_AMD_K4_RING")) {
             const unsigned long v = strtoul(e, nullptr, 10);
             if (v >= 4096 && v <= 65536 && (v & (v - 1)) == 0) cap = (uint32_t)v;

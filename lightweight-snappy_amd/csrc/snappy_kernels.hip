@@ -979,11 +979,13 @@ __device__ __forceinline__ void k4_flush(const uint8_t *ob, uint32_t M, uint8_t 
         if (a > T) a = T;
         if (F + lane < a) dst[F + lane] = ob[(F + lane) & M];
         const uint32_t e = T & ~15u;
+#pragma unroll 1
         for (uint32_t x = a + 16 * lane; x < e; x += 1024)
             *reinterpret_cast<u32x4 *>(dst + x) = *reinterpret_cast<const u32x4 *>(ob + (x & M));
         const uint32_t t0 = e > a ? e : a;
         if (t0 + lane < T) dst[t0 + lane] = ob[(t0 + lane) & M];
     } else {
+#pragma unroll 1
         for (uint32_t x = F + lane; x < T; x += 64) dst[x] = ob[x & M];
     }
 }
@@ -1171,6 +1173,7 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
                 // everything before the literal goes out first; the literal is
                 // written to HBM and to the ring (later copies read its tail)
                 k4_flush(ob, M, dst, F, kop, lane);
+#pragma unroll 1
                 for (uint32_t b = 0; b < kl; b += 256) {
                     uint8_t v[4];
 #pragma unroll

@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--bytes-per-gpu", type=int, default=1 << 30)
     ap.add_argument("--assemble", action="store_true", help="also time the RCCL all-gather of shards")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-e2e", action="store_true", help="skip the PCIe-inclusive host API sample")
     ap.add_argument("--cpu-sample-bytes", type=int, default=1 << 30)
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="rocprofv3 PMC summary giving HBM traffic per launch (see profiles/README.md)")
@@ -88,10 +89,74 @@ def cpu_baseline(kind: str, seed: int, chunk: int, layout: int, sample: int) -> 
                 break
     except OSError:
         pass
-    return {"value": round(a.size / (t2 - t0) / 1e6, 2), "unit": "MB/s", "cores": 1, "kind": "port",
+    base = {"value": round(a.size / (t2 - t0) / 1e6, 2), "unit": "MB/s", "cores": 1, "kind": "port",
             "sample": f"{a.size / 2**20:.0f} MiB of the same workload, compress {a.size / (t1 - t0) / 1e6:.1f} MB/s"
                       f" + decompress {a.size / (t2 - t1) / 1e6:.1f} MB/s, oracle/snappy_oracle.c -O2, 1 thread,"
                       f" {cpu_model}"}
+    # all host cores of this box's share over independent units
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
+    t0 = time.perf_counter()
+    if layout == snappy_amd.STREAMS:
+        payload, offs = oracle.compress_streams(a, chunk, threads=threads)
+        t1 = time.perf_counter()
+        back = oracle.decompress_streams(payload, offs, a.size, chunk, threads=threads)
+    else:  # independent 64 KiB blocks: the all-core upper bound of the reference algorithm
+        payload, offs = oracle.compress_streams(a, 65536, threads=threads)
+        t1 = time.perf_counter()
+        back = oracle.decompress_streams(payload, offs, a.size, 65536, threads=threads)
+    t2 = time.perf_counter()
+    assert np.array_equal(back, a)
+    allc = {"value": round(a.size / (t2 - t0) / 1e6, 2), "unit": "MB/s", "cores": threads, "kind": "port",
+            "compress_MBps": round(a.size / (t1 - t0) / 1e6, 1),
+            "decompress_MBps": round(a.size / (t2 - t1) / 1e6, 1)}
+    return base, allc
+
+
+def host_end_to_end(kind: str, seed: int, sample: int) -> dict:
+    """PCIe-inclusive rate of the drop-in host API (snappy_compress_buffer /
+    snappy_decompress_buffer: one SINGLE stream of 64 KiB blocks, pageable
+    host buffers in and out).  Reported beside `value`, never as it."""
+    import ctypes
+    lib = snappy_amd.lib()
+    a = datagen.make(kind, sample, seed)
+    cap = snappy_amd.max_compressed_length(a.size)
+    comp = np.empty(cap, dtype=np.uint8)
+    back = np.empty(a.size, dtype=np.uint8)
+    got = ctypes.c_size_t(0)
+    vp = ctypes.c_void_p
+    best_c = best_d = float("inf")
+    for _ in range(3):
+        t0 = time.perf_counter()
+        rc = lib.snappy_compress_buffer(vp(a.ctypes.data), a.size, vp(comp.ctypes.data), ctypes.byref(got))
+        t1 = time.perf_counter()
+        assert rc == 0, rc
+        clen = got.value
+        rc = lib.snappy_decompress_buffer(vp(comp.ctypes.data), clen, vp(back.ctypes.data), a.size,
+                                          ctypes.byref(got))
+        t2 = time.perf_counter()
+        assert rc == 0 and got.value == a.size, rc
+        best_c, best_d = min(best_c, t1 - t0), min(best_d, t2 - t1)
+    assert np.array_equal(back, a)
+    return {"bytes": int(a.size), "layout": "SINGLE 64 KiB blocks", "compress_MBps": round(a.size / best_c / 1e6, 1),
+            "decompress_MBps": round(a.size / best_d / 1e6, 1), "note": "pageable host buffers, H2D+D2H included"}
+
+
+def hbm_copy_gbps(dev, nbytes: int = 1 << 30) -> float:
+    """Device-to-device copy (read + write bytes) as the box's HBM check."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize(dev)
+    best = float("inf")
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        e1.synchronize()
+        best = min(best, e0.elapsed_time(e1) * 1e-3)
+    del a, b
+    return round(2 * nbytes / best / 1e9, 1)
 
 
 def main():
@@ -182,6 +247,7 @@ def main():
         assemble = {"allgather_ms": round(tb * 1e3, 3), "bytes": int(world * mx),
                     "GBps_per_rank_in": round((world - 1) * mx / tb / 1e9, 2)}
 
+    hbm_gbps = hbm_copy_gbps(dev) if rank == 0 else None
     total_in = n * world
     ms_step = elapsed / args.steps * 1e3
     value = total_in / (elapsed / args.steps) / 1e6
@@ -202,9 +268,11 @@ def main():
         pass
 
     if rank == 0:
-        cpu = None
+        cpu = cpu_all = e2e = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(kind, seed, chunk, layout, min(args.cpu_sample_bytes, n))
+            cpu, cpu_all = cpu_baseline(kind, seed, chunk, layout, min(args.cpu_sample_bytes, n))
+        if world == 1 and not args.no_host_e2e:
+            e2e = host_end_to_end(kind, seed, min(n, 256 << 20))
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
@@ -217,9 +285,14 @@ def main():
                          "kernel": dom_name, "kernel_ms": round(dom_ms, 3),
                          "algorithmic_bytes_per_launch": dom_bytes},
             "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_all,
             "ratio": round(total_in / total_comp, 4),
             "compress_MBps": round(n / ((k1m + k3m) * 1e-3) / 1e6, 1),
             "decompress_MBps": round(n / (k4m * 1e-3) / 1e6, 1),
+            # src/result.c:40 defines decompress speed over the compressed bytes
+            "decompress_MBps_ref_definition": round(comp_bytes / (k4m * 1e-3) / 1e6, 1),
+            "hbm_copy_GBps_measured": hbm_gbps,
+            "host_end_to_end": e2e,
             "kernel_ms": {"k1_match": round(k1m, 3), "k3_scan_k2_emit": round(k3m, 3),
                           "k4_decode": round(k4m, 3)},
             "hbm_frac": {"compress_k1": round((n + comp_bytes) / (k1m * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),

@@ -11,8 +11,8 @@ export TMPDIR=/tmp
 STEPS=${STEPS:-5}
 timeout -k 10 400 python bench.py --steps $STEPS --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o run --output-format csv -- \
-    python3 bench.py --steps $STEPS --warmup 2 --no-cpu-baseline > gpurun_out/prof_trace.log 2>&1 &&
+    python3 bench.py --steps $STEPS --warmup 2 --no-cpu-baseline --no-host-e2e > gpurun_out/prof_trace.log 2>&1 &&
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/prof_fetch -o run --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof_fetch.log 2>&1 &&
+    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-e2e > gpurun_out/prof_fetch.log 2>&1 &&
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/prof_write -o run --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof_write.log 2>&1
+    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-e2e > gpurun_out/prof_write.log 2>&1

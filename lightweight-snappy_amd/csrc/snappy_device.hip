@@ -38,6 +38,7 @@ struct snappy_amd_ctx {
     uint8_t *d_a = nullptr; size_t d_a_cap = 0;
     uint8_t *d_b = nullptr; size_t d_b_cap = 0;
     uint64_t *d_idx = nullptr; size_t d_idx_cap = 0;
+    uint8_t *k5buf = nullptr; size_t k5buf_cap = 0;  // chunk-parallel index scratch
     bool timing = false;
     hipEvent_t ev[5] = {};
     float k1_ms = 0, k3_ms = 0, k4_ms = 0;
@@ -111,7 +112,8 @@ void snappy_amd_destroy(snappy_amd_ctx *c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void *bufs[] = {c->scratch, c->sizes, c->tokens, c->ntok, c->status, c->total, c->k5res, c->d_a, c->d_b, c->d_idx};
+    void *bufs[] = {c->scratch, c->sizes, c->tokens, c->ntok, c->status, c->total, c->k5res, c->d_a, c->d_b, c->d_idx,
+                    c->k5buf};
     for (void *b : bufs) if (b) (void)hipFree(b);
     if (c->h_total) (void)hipHostFree(c->h_total);
     if (c->h_status) (void)hipHostFree(c->h_status);
@@ -339,8 +341,28 @@ int snappy_amd_index_device(snappy_amd_ctx *c, const void *d_comp, size_t clen, 
 {
     if (!c || !d_comp || !d_offsets) return SNAPPY_AMD_ERR_ARG;
     HIP_OK(hipSetDevice(c->device));
-    hipLaunchKernelGGL(k5_index_stream, dim3(1), dim3(64), 0, c->stream, static_cast<const uint8_t *>(d_comp),
-                       (uint64_t)clen, d_offsets, (uint64_t)max_units, c->k5res);
+    const uint8_t *comp = static_cast<const uint8_t *>(d_comp);
+    const bool serial = getenv("SNAPPY_AMD_K5_SERIAL") != nullptr;  // read per call (tests toggle it)
+    if (serial || clen < 4 * (size_t)K5_CHUNK || (reinterpret_cast<uintptr_t>(d_comp) & 3)) {
+        hipLaunchKernelGGL(k5_index_stream, dim3(1), dim3(64), 0, c->stream, comp, (uint64_t)clen, d_offsets,
+                           (uint64_t)max_units, c->k5res);
+    } else {
+        // chunk-parallel walk (K5a..K5d); chunk c covers [hdr + c*K5_CHUNK, +K5_CHUNK)
+        const uint32_t nch = (uint32_t)((clen + K5_CHUNK - 1) / K5_CHUNK);
+        const size_t per = 2 * 64 * 8 + 2 * 8 + 4;
+        int rc = grow(reinterpret_cast<void **>(&c->k5buf), &c->k5buf_cap, per * nch + 64);
+        if (rc) return rc;
+        uint64_t *X = reinterpret_cast<uint64_t *>(c->k5buf);
+        uint64_t *O = X + 64 * (size_t)nch, *Ent = O + 64 * (size_t)nch, *Base = Ent + nch, *fin = Base + nch;
+        int32_t *cst = reinterpret_cast<int32_t *>(fin + 8);
+        hipLaunchKernelGGL(k5a_chunk_walk, dim3(nch), dim3(64), 0, c->stream, comp, (uint64_t)clen, X, O);
+        hipLaunchKernelGGL(k5b_carry, dim3(1), dim3(64), 0, c->stream, comp, (uint64_t)clen, nch, X, O, Ent, Base,
+                           c->k5res);
+        hipLaunchKernelGGL(k5c_mark, dim3(nch), dim3(64), 0, c->stream, comp, (uint64_t)clen, Ent, Base, d_offsets,
+                           (uint64_t)max_units, cst, fin);
+        hipLaunchKernelGGL(k5d_result, dim3(1), dim3(64), 0, c->stream, nch, cst, c->k5res, d_offsets,
+                           (uint64_t)max_units);
+    }
     HIP_OK(hipGetLastError());
     int64_t res[3];
     HIP_OK(hipMemcpyAsync(res, c->k5res, sizeof(res), hipMemcpyDeviceToHost, c->stream));

@@ -55,6 +55,17 @@ __global__ void k4_decompress_units(const uint8_t *__restrict__ comp, const uint
                                     uint64_t n, uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
                                     uint32_t comp_cap, uint32_t ring,
                                     uint8_t *__restrict__ out, int32_t *__restrict__ status);
+constexpr uint32_t K5_CHUNK = 16384;  // == K5_S in the kernels
+__global__ void k5a_chunk_walk(const uint8_t *__restrict__ comp, uint64_t clen, uint64_t *__restrict__ X,
+                               uint64_t *__restrict__ O);
+__global__ void k5b_carry(const uint8_t *__restrict__ comp, uint64_t clen, uint32_t nchunks,
+                          const uint64_t *__restrict__ X, const uint64_t *__restrict__ O, uint64_t *__restrict__ Ent,
+                          uint64_t *__restrict__ Base, int64_t *__restrict__ result);
+__global__ void k5c_mark(const uint8_t *__restrict__ comp, uint64_t clen, const uint64_t *__restrict__ Ent,
+                         const uint64_t *__restrict__ Base, uint64_t *__restrict__ offsets, uint64_t max_units,
+                         int32_t *__restrict__ cst, uint64_t *__restrict__ fin);
+__global__ void k5d_result(uint32_t nchunks, const int32_t *__restrict__ cst, int64_t *__restrict__ result,
+                           uint64_t *__restrict__ offsets, uint64_t max_units);
 __global__ void k5_index_stream(const uint8_t *__restrict__ comp, uint64_t clen, uint64_t *__restrict__ offsets,
                                 uint64_t max_units, int64_t *__restrict__ result);
 

@@ -1401,6 +1401,263 @@ __global__ __launch_bounds__(64) void k5_index_stream(const uint8_t *__restrict_
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// K5p: block index of a foreign SINGLE stream, chunk-parallel.  A stream has
+// no block markers (the decoder of src/snappy_decompression.c:345-363 just
+// walks elements until 65,536 bytes came out), so the walk is split into
+// K5_S-byte chunks of compressed stream:
+//   K5a  every chunk walks speculatively from its first byte, keeping the
+//        first 64 element starts it visits (with the output before each),
+//        its exit (first start at or past the chunk end) and its output;
+//   K5b1 chunk c checks whether the exit of chunk c-1 is one of its visited
+//        starts (element chains through the same bytes coincide from the
+//        first common start on);
+//   K5b2 one wave carries the true entry and output base through the chunks
+//        (hypothesis hits cost a few SALU ops, misses walk serially);
+//   K5c  every chunk re-walks from its true entry with the true output base
+//        and records the element starts where the output reaches a multiple
+//        of 65,536 (with the checks of K5);
+//   K5d  first error in stream order, final offset.
+// Chunks entirely inside one element (long literals) are skipped.
+// ---------------------------------------------------------------------------
+constexpr uint32_t K5_S = 16384;
+constexpr uint64_t K5_SKIP = ~0ull;
+
+struct K5Hdr {
+    uint64_t N;
+    uint32_t len;
+    int32_t st;
+};
+
+__device__ __forceinline__ K5Hdr k5_header(const uint8_t *comp, uint64_t clen)
+{
+    K5Hdr h{0, 0, SNAPPY_ST_HEADER};
+    for (uint32_t k = 0; k < 10 && k < clen; k++) {
+        const uint32_t b = comp[k];
+        h.N |= (uint64_t)(b & 0x7F) << (7 * k);
+        if (!(b & 0x80)) {
+            h.len = k + 1;
+            h.st = SNAPPY_ST_OK;
+            break;
+        }
+    }
+    return h;
+}
+
+// element at x: compressed size and output length; false if its header
+// bytes run past clen (uniform across the wave: scalar loads)
+__device__ __forceinline__ bool k5_parse(const uint8_t *__restrict__ comp, uint64_t clen, uint64_t x, uint64_t &size,
+                                         uint64_t &len)
+{
+    uint64_t v;  // bytes x .. x+4 (little-endian), zero past clen
+    if (x + 8 <= clen) {
+        const uint64_t a = x & ~3ull;
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(comp + a);
+        const uint64_t d = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+        const uint32_t sh = 8 * (uint32_t)(x & 3);
+        v = d >> sh;
+        if (sh > 24) v |= (uint64_t)comp[x + 4] << 32;
+        else v &= 0xFFFFFFFFFFull;
+    } else {
+        if (x >= clen) return false;
+        v = 0;
+        for (uint32_t k = 0; k < 5; k++)
+            if (x + k < clen) v |= (uint64_t)comp[x + k] << (8 * k);
+    }
+    const uint32_t tag = (uint32_t)v & 0xFF;
+    uint32_t hb;  // header bytes
+    switch (tag & 3) {
+    case 0: {
+        const uint32_t m = tag >> 2;
+        if (m < 60) {
+            len = m + 1;
+            hb = 1;
+        } else {
+            const uint32_t k = m - 59;
+            len = ((v >> 8) & (k == 4 ? 0xFFFFFFFFull : ((1ull << (8 * k)) - 1))) + 1;
+            hb = 1 + k;
+        }
+        size = hb + len;
+        break;
+    }
+    case 1: len = ((tag >> 2) & 7) + 4; hb = 2; size = 2; break;
+    case 2: len = (tag >> 2) + 1; hb = 3; size = 3; break;
+    default: len = (tag >> 2) + 1; hb = 5; size = 5; break;
+    }
+    return x + hb <= clen;
+}
+
+__global__ __launch_bounds__(64) void k5a_chunk_walk(const uint8_t *__restrict__ comp, uint64_t clen,
+                                                     uint64_t *__restrict__ X, uint64_t *__restrict__ O)
+{
+    // lane l walks from byte l of the chunk: every entry offset < 64 is
+    // covered exactly (no reliance on chains converging; a periodic stream
+    // never re-synchronises)
+    const uint32_t lane = threadIdx.x;
+    const uint32_t c = blockIdx.x;
+    const K5Hdr h = k5_header(comp, clen);
+    const uint64_t c0 = h.len + (uint64_t)c * K5_S;
+    const uint64_t end = c0 + K5_S < clen ? c0 + K5_S : clen;
+    uint64_t x = c0 + lane, cum = 0;
+    while (x < end) {
+        uint64_t size, len;
+        if (!k5_parse(comp, clen, x, size, len)) {
+            x = clen + 1;
+            break;
+        }
+        cum += len;
+        x += size;
+    }
+    X[(uint64_t)c * 64 + lane] = x;
+    O[(uint64_t)c * 64 + lane] = cum;
+}
+
+// 64-bit readlane
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l)
+{
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+
+constexpr uint32_t K5_G = 8;  // chunks per prefetch group
+
+__global__ __launch_bounds__(64) void k5b_carry(const uint8_t *__restrict__ comp, uint64_t clen, uint32_t nchunks,
+                                                const uint64_t *__restrict__ X, const uint64_t *__restrict__ O,
+                                                uint64_t *__restrict__ Ent, uint64_t *__restrict__ Base,
+                                                int64_t *__restrict__ result)
+{
+    const uint32_t lane = threadIdx.x;
+    const K5Hdr h = k5_header(comp, clen);
+    const uint64_t N = h.N;
+    uint64_t E = h.len, base = 0;
+    uint64_t xa[K5_G], oa[K5_G], xb[K5_G], ob_[K5_G];
+    auto load = [&](uint32_t g, uint64_t *xs, uint64_t *os) {
+#pragma unroll
+        for (uint32_t j = 0; j < K5_G; j++) {
+            const uint64_t c = (uint64_t)g * K5_G + j;
+            xs[j] = c < nchunks ? X[c * 64 + lane] : 0;
+            os[j] = c < nchunks ? O[c * 64 + lane] : 0;
+        }
+    };
+    auto run = [&](uint32_t g, const uint64_t *xs, const uint64_t *os) {
+#pragma unroll
+        for (uint32_t j = 0; j < K5_G; j++) {
+            const uint32_t c = g * K5_G + j;
+            if (c >= nchunks) break;
+            const uint64_t c0 = h.len + (uint64_t)c * K5_S;
+            const uint64_t end = c0 + K5_S < clen ? c0 + K5_S : clen;
+            if (h.st != SNAPPY_ST_OK || base >= N || E >= end) {
+                if (lane == 0) Ent[c] = K5_SKIP;
+                continue;
+            }
+            if (lane == 0) {
+                Ent[c] = E;
+                Base[c] = base;
+            }
+            if (E - c0 < 64) {
+                const uint32_t l = (uint32_t)(E - c0);
+                base += rl64(os[j], l);
+                E = rl64(xs[j], l);
+            } else {  // entered past byte 63 (after a long literal): walk the chunk
+                uint64_t x = E;
+                while (x < end && base < N) {
+                    uint64_t size, len;
+                    if (!k5_parse(comp, clen, x, size, len)) {
+                        x = clen + 1;
+                        break;
+                    }
+                    base += len;
+                    x += size;
+                }
+                E = x;
+            }
+        }
+    };
+    const uint32_t ng = (nchunks + K5_G - 1) / K5_G;
+    load(0, xa, oa);
+    for (uint32_t g = 0; g < ng; g += 2) {
+        load(g + 1, xb, ob_);
+        run(g, xa, oa);
+        load(g + 2, xa, oa);
+        run(g + 1, xb, ob_);
+    }
+    if (lane == 0) {
+        result[0] = h.st;
+        result[1] = (int64_t)N;
+        result[2] = (int64_t)base;  // output the chain accounts for (== N for a whole stream)
+    }
+}
+
+__global__ __launch_bounds__(64) void k5c_mark(const uint8_t *__restrict__ comp, uint64_t clen,
+                                               const uint64_t *__restrict__ Ent, const uint64_t *__restrict__ Base,
+                                               uint64_t *__restrict__ offsets, uint64_t max_units,
+                                               int32_t *__restrict__ cst, uint64_t *__restrict__ fin)
+{
+    const uint32_t lane = threadIdx.x;
+    const uint32_t c = blockIdx.x;
+    const K5Hdr h = k5_header(comp, clen);
+    int32_t st = SNAPPY_ST_OK;
+    uint64_t x = Ent[c];
+    if (x != K5_SKIP) {
+        const uint64_t N = h.N;
+        const uint64_t units = (N + SNAPPY_BLOCK - 1) / SNAPPY_BLOCK;
+        const uint64_t c0 = h.len + (uint64_t)c * K5_S;
+        const uint64_t end = c0 + K5_S < clen ? c0 + K5_S : clen;
+        uint64_t op = Base[c];
+        while (x < end && op < N) {
+            uint64_t size, len;
+            if (!k5_parse(comp, clen, x, size, len) || x + size > clen) {
+                st = SNAPPY_ST_TRUNCATED;
+                break;
+            }
+            const uint64_t nb = (op / SNAPPY_BLOCK + 1) * SNAPPY_BLOCK;  // element must not straddle a block
+            if (op + len > nb && nb < N) {
+                st = SNAPPY_ST_UNSUPPORTED;
+                break;
+            }
+            op += len;
+            x += size;
+            if (op > N) {
+                st = SNAPPY_ST_OVERRUN;
+                break;
+            }
+            if ((op & (SNAPPY_BLOCK - 1)) == 0 && op < N && lane == 0) {
+                const uint64_t u = op / SNAPPY_BLOCK;
+                if (u < max_units) offsets[u] = x;
+            }
+        }
+        if (st == SNAPPY_ST_OK && op == N && lane == 0) {
+            if (units < max_units) offsets[units] = x;
+            *fin = x;
+        }
+        if (st == SNAPPY_ST_OK && op < N && x >= clen) st = SNAPPY_ST_TRUNCATED;
+    }
+    if (lane == 0) cst[c] = st;
+}
+
+__global__ __launch_bounds__(64) void k5d_result(uint32_t nchunks, const int32_t *__restrict__ cst,
+                                                 int64_t *__restrict__ result, uint64_t *__restrict__ offsets,
+                                                 uint64_t max_units)
+{
+    const uint32_t lane = threadIdx.x;
+    int64_t st = result[0];
+    const uint64_t N = (uint64_t)result[1];
+    const uint64_t units = (N + SNAPPY_BLOCK - 1) / SNAPPY_BLOCK;
+    if (st == SNAPPY_ST_OK && units > max_units) st = SNAPPY_ST_CAPACITY;
+    for (uint32_t cb = 0; st == SNAPPY_ST_OK && cb < nchunks; cb += 64) {
+        const int32_t v = cb + lane < nchunks ? cst[cb + lane] : 0;
+        const uint64_t m = __ballot(v != SNAPPY_ST_OK);
+        if (m) st = __builtin_amdgcn_readlane(v, (uint32_t)__builtin_ctzll(m));
+    }
+    if (st == SNAPPY_ST_OK && (uint64_t)result[2] < N) st = SNAPPY_ST_TRUNCATED;
+    if (lane == 0) {
+        if (st == SNAPPY_ST_OK && units) offsets[0] = 0;
+        result[0] = st;
+        result[2] = (int64_t)units;
+    }
+}
+
 }  // namespace snappy_amd
 
 #ifdef SNAPPY_K4_STATS

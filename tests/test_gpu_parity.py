@@ -174,3 +174,58 @@ def test_full_size_extremes_1gib(codec, kind, seed):
     assert cpre.cpu().numpy().tobytes() == oracle.compress(pre.tobytes())
     back = codec.decompress_tensor(comp, offs, n, layout=snappy_amd.SINGLE)
     assert torch.equal(back, to_dev(a))
+
+
+def _index_both(codec, d):
+    """(code, n, offsets) from the chunk-parallel K5p and from the serial K5."""
+    res = []
+    for serial in (False, True):
+        if serial:
+            os.environ["SNAPPY_AMD_K5_SERIAL"] = "1"
+        try:
+            n, offs = codec.index_tensor(d)
+            res.append((0, n, offs.cpu().numpy().copy()))
+        except snappy_amd.SnappyError as e:
+            res.append((e.code, None, None))
+        finally:
+            os.environ.pop("SNAPPY_AMD_K5_SERIAL", None)
+    return res
+
+
+def test_parallel_index_matches_serial_and_compressor(codec):
+    # K5p (chunk-parallel boundary finder) vs the serial K5 walk vs the block
+    # index the compressor itself produced, on streams whose elements cross
+    # chunk edges in every way: text, all-literal (65,536-byte literals span
+    # four chunks), all-copy, and a mix with zero runs
+    rng = np.random.default_rng(5)
+    mixed = np.concatenate([datagen.make("T", 3 << 20, 9), datagen.make("R", 1 << 20, 3),
+                            np.zeros(777_777, np.uint8), datagen.make("P", 1 << 20, 4),
+                            rng.integers(0, 4, 500_001, dtype=np.uint8), datagen.make("T", 2 << 20, 10)])
+    for a in (datagen.make("T", 24 << 20, 21), datagen.make("R", 6 << 20, 1), datagen.make("P", 6 << 20, 2), mixed):
+        x = to_dev(a)
+        comp, offs = codec.compress_tensor(x, chunk=snappy_amd.BLOCK, layout=snappy_amd.SINGLE)
+        want = offs.cpu().numpy()
+        (c1, n1, o1), (c2, n2, o2) = _index_both(codec, comp)
+        assert c1 == 0 and c2 == 0
+        assert n1 == n2 == a.size
+        assert np.array_equal(o1, want) and np.array_equal(o2, want)
+
+
+def test_parallel_index_errors_match_serial(codec):
+    import torch
+    a = datagen.make("T", 6 << 20, 33)
+    comp, _ = codec.compress_tensor(to_dev(a), chunk=snappy_amd.BLOCK, layout=snappy_amd.SINGLE)
+    raw = comp.cpu().numpy()
+    rng = np.random.default_rng(7)
+    cases = [raw[:-1], raw[: raw.size // 2], raw[: raw.size - 70000]]
+    for _ in range(6):  # byte flips in the middle: error or a different but consistent parse
+        b = raw.copy()
+        pos = rng.integers(1 << 16, raw.size - (1 << 16), 4)
+        b[pos] ^= rng.integers(1, 255, 4, dtype=np.uint8)
+        cases.append(b)
+    for b in cases:
+        d = torch.from_numpy(np.ascontiguousarray(b)).cuda()
+        (c1, n1, o1), (c2, n2, o2) = _index_both(codec, d)
+        assert c1 == c2
+        if c1 == 0:
+            assert n1 == n2 and np.array_equal(o1, o2)

@@ -495,7 +495,21 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
                                                           uint32_t *__restrict__ sizes)
 {
     constexpr int W = SNAPPY_K1R_WINDOW;
+#ifndef SNAPPY_K1R_TABLE16
+    // 12 KiB: u16 positions + u8 tags: 12 units/CU (the VGPR limit) instead of
+    // 10 with u32 entries
+    __shared__ uint16_t tpos[kTable];
+    __shared__ uint8_t ttag[kTable];
+#define TAG_OF(v) (((v) * kTagMul) >> 24)
+#define TBL_READ(h) ((uint32_t)tpos[h] | ((uint32_t)ttag[h] << 16))
+#define TBL_WRITE(s, word) do { const uint32_t _w = (word); tpos[s] = (uint16_t)_w; ttag[s] = (uint8_t)(_w >> 16); } while (0)
+#else
+    // 16 KiB: u32 entries, position | 16-bit tag << 16
     __shared__ uint32_t table[kTable];
+#define TAG_OF(v) (((v) * kTagMul) >> 16)
+#define TBL_READ(h) table[h]
+#define TBL_WRITE(s, word) table[s] = (word)
+#endif
     const uint32_t lane = threadIdx.x;
     const uint32_t u = blockIdx.x;
     const uint64_t base = (uint64_t)u * unit;
@@ -534,8 +548,8 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
 
     // never-set slots mean position 0 (snappy_compression.c:259-265): tag of BE32(0)
     const uint32_t cur0 = BE32_REG(0);
-    const uint32_t init = ((cur0 * kTagMul) >> 16) << 16;
-    for (uint32_t i = lane; i < kTable; i += 64) table[i] = init;
+    const uint32_t init = TAG_OF(cur0) << 16;
+    for (uint32_t i = lane; i < kTable; i += 64) TBL_WRITE(i, init);
     __syncthreads();
 
     uint2 *tok = tokens + (uint64_t)u * tok_cap;
@@ -556,7 +570,7 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
         const uint32_t _b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_k + 1) << 2), (int)_w); \
         const uint32_t _s = 8 * ((q0 + lane) & 3);                                                 \
         bv = _s ? (_a << _s) | (_b >> (32 - _s)) : _a;                                             \
-        hv = ((bv * kMul) >> shift) | (((bv * kTagMul) >> 16) << 16);                              \
+        hv = ((bv * kMul) >> shift) | (TAG_OF(bv) << 16);                                          \
     } while (0)
 
 #ifdef SNAPPY_K1R_STATS
@@ -590,7 +604,7 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
         const uint32_t h = hvp & 0xFFFF, a = hvq & 0xFFFF;
         STAMP(s2);
         SEG(1, s1, s2);
-        const uint32_t ent = table[h];
+        const uint32_t ent = TBL_READ(h);
 #ifdef SNAPPY_K1R_EARLY_READ
         __builtin_amdgcn_sched_barrier(0);  // issue the table read before the conflict math
 #endif
@@ -604,8 +618,8 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
         SEG(2, s2, s3);
         // lanes before f are exact misses: update_hash_table :303-307
         if (lane < f) {
-            table[a] = (pk - 1) | (hvq & 0xFFFF0000u);
-            table[h] = pk | (hvp & 0xFFFF0000u);
+            TBL_WRITE(a, (pk - 1) | (hvq & 0xFFFF0000u));
+            TBL_WRITE(h, pk | (hvp & 0xFFFF0000u));
         }
         const uint64_t hits = __ballot((hit & ~(inval | conflict)) != 0);
         STAMP(s4);
@@ -680,7 +694,7 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
                 tkb = (uint32_t)amdgcn_writelane((int)off, (int)(nt & 63), (int)tkb);
                 nt++;
                 if ((nt & 63) == 0) tok[nt - 64 + lane] = make_uint2(tka, tkb);
-                table[hf & 0xFFFF] = pf | (hf & 0xFFFF0000u);  // emit_copy :328
+                TBL_WRITE(hf & 0xFFFF, pf | (hf & 0xFFFF0000u));  // emit_copy :328
                 skip = 32;
                 p = pf + len;
 #ifdef SNAPPY_K1R_MSTAMPS
@@ -694,8 +708,8 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
             }
             // tag collision: lane f is a miss as well
             const uint32_t af = __builtin_amdgcn_readlane(hvq, f);
-            table[af & 0xFFFF] = (pf - 1) | (af & 0xFFFF0000u);
-            table[hf & 0xFFFF] = pf | (hf & 0xFFFF0000u);
+            TBL_WRITE(af & 0xFFFF, (pf - 1) | (af & 0xFFFF0000u));
+            TBL_WRITE(hf & 0xFFFF, pf | (hf & 0xFFFF0000u));
             next_f = f + 1;
         }
         // f (or f + 1) misses consumed; f stops at a conflict, the window
@@ -706,6 +720,9 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
         SEG(4, s4, s5);
     }
 #undef WINDOW_AT
+#undef TAG_OF
+#undef TBL_READ
+#undef TBL_WRITE
     (void)sizes;
     if (lane < (nt & 63)) tok[(nt & ~63u) + lane] = make_uint2(tka, tkb);
     if (lane == 0) ntok_out[u] = nt;

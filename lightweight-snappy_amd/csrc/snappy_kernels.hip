@@ -557,17 +557,21 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
     uint32_t nt = 0;
 
     // position window: lane l <-> position q0 + l
-    uint32_t q0 = 0xFFFFFFFFu, hv = 0, bv = 0, dv = 0;
-// lane l <- BE32 at q0 + l (from dwords q0/4 + k, k = ((q0 & 3) + l) / 4 <= 16);
-// dv keeps the dwords q0/4 + l themselves (the match side of a verification)
+    uint32_t q0 = 0xFFFFFFFFu, hv = 0, bv = 0, dv = 0, d0 = 0xFFFF0000u;  // d0: forces the first refresh
+// dv: lane l <- dword d0 + l (256 bytes, refreshed when q0 / 4 leaves
+// [d0, d0 + 34], which keeps both the position window and a match's 16
+// verification dwords inside it); position window: lane l <- BE32 at q0 + l
+// (from dwords q0/4 + k, k = ((q0 & 3) + l) / 4 <= 16)
 #define WINDOW_AT(qq)                                                                              \
     do {                                                                                           \
         q0 = (qq);                                                                                 \
-        dv = DW_LANES(q0 >> 2);                                                                    \
-        const uint32_t _w = dv;                                                                    \
-        const uint32_t _k = ((q0 & 3) + lane) >> 2;                                                \
-        const uint32_t _a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_k << 2), (int)_w);       \
-        const uint32_t _b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_k + 1) << 2), (int)_w); \
+        if ((q0 >> 2) - d0 > 34) {                                                                 \
+            d0 = q0 >> 2;                                                                          \
+            dv = DW_LANES(d0);                                                                     \
+        }                                                                                          \
+        const uint32_t _k = (q0 >> 2) - d0 + (((q0 & 3) + lane) >> 2);                            \
+        const uint32_t _a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_k << 2), (int)dv);       \
+        const uint32_t _b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_k + 1) << 2), (int)dv); \
         const uint32_t _s = 8 * ((q0 + lane) & 3);                                                 \
         bv = _s ? (_a << _s) | (_b >> (32 - _s)) : _a;                                             \
         hv = ((bv * kMul) >> shift) | (TAG_OF(bv) << 16);                                          \
@@ -593,10 +597,17 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
         SEG(0, s0, s1);
         // ---- speculative window: lane k = k-th probe if all earlier miss
         const uint32_t sk = skip + lane;
-        const uint32_t pk = p + skipsum(sk) - skipsum(skip);
+        uint32_t pk, bend;  // probe position, is_block_end bound (skip >> 5) + 15
+        if (skip <= 64 - W) {  // every speculative lane steps by 1 (after a match: skip = 32)
+            pk = p + lane;
+            bend = 16;
+        } else {
+            pk = p + skipsum(sk) - skipsum(skip);
+            bend = (sk >> 5) + 15;
+        }
         // invalid: lane >= W, block end (is_block_end), or past the window
         const uint32_t inval = (uint32_t)(((int32_t)(W - 1 - lane)) >> 31) |
-                               (uint32_t)(((int32_t)(L - pk) - (int32_t)((sk >> 5) + 15)) >> 31) |
+                               (uint32_t)(((int32_t)(L - pk) - (int32_t)bend) >> 31) |
                                (uint32_t)(((int32_t)(q0 + 64) - (int32_t)(pk + 12)) >> 31);
         const uint32_t ik = inval ? 1 : pk - q0;
         const uint32_t hvp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ik << 2), (int)hv);
@@ -641,8 +652,8 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
             const uint32_t hf = __builtin_amdgcn_readlane(hvp, f);
             // lanes 0..15 compare BE32 at pf + 4j and cand + 4j: verification
             // (first 4 bytes) and find_copy_length :61-72 up to 64 bytes at once
-            // pf side from the dword window (pf <= q0 + 52, so dword index <= 30)
-            const uint32_t kp = (pf >> 2) - (q0 >> 2) + (lane & 15);
+            // pf side from the dword window (pf <= q0 + 52 and q0 / 4 - d0 <= 34: index <= 63)
+            const uint32_t kp = (pf >> 2) - d0 + (lane & 15);
             const uint32_t pa = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(kp << 2), (int)dv);
             const uint32_t pb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((kp + 1) << 2), (int)dv);
             const uint32_t ps = 8 * (pf & 3);
@@ -714,7 +725,7 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
         }
         // f (or f + 1) misses consumed; f stops at a conflict, the window
         // edge or the block end and is retried exactly as the next lane 0
-        p = p + skipsum(skip + next_f) - skipsum(skip);
+        p = skip + next_f <= 64 ? p + next_f : p + skipsum(skip + next_f) - skipsum(skip);
         skip += next_f;
         STAMP(s5);
         SEG(4, s4, s5);

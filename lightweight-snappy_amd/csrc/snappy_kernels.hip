@@ -577,6 +577,17 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
         hv = ((bv * kMul) >> shift) | (TAG_OF(bv) << 16);                                          \
     } while (0)
 
+// lanes 0..15 <- BE32 at pp + 4*lane from the dword window
+#define PV_LANES16(pp)                                                                             \
+    ({                                                                                             \
+        const uint32_t _pp = (pp);                                                                 \
+        const uint32_t _kp = (_pp >> 2) - d0 + (lane & 15);                                        \
+        const uint32_t _pa = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_kp << 2), (int)dv);     \
+        const uint32_t _pb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_kp + 1) << 2), (int)dv); \
+        const uint32_t _ps = 8 * (_pp & 3);                                                        \
+        _ps ? (_pa << _ps) | (_pb >> (32 - _ps)) : _pa;                                            \
+    })
+
 #ifdef SNAPPY_K1R_STATS
     const uint64_t t_loop = clock64();
     uint32_t n_probe = 0, n_match = 0, n_round = 0;
@@ -653,12 +664,7 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
             // lanes 0..15 compare BE32 at pf + 4j and cand + 4j: verification
             // (first 4 bytes) and find_copy_length :61-72 up to 64 bytes at once
             // pf side from the dword window (pf <= q0 + 52 and q0 / 4 - d0 <= 34: index <= 63)
-            const uint32_t kp = (pf >> 2) - d0 + (lane & 15);
-            const uint32_t pa = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(kp << 2), (int)dv);
-            const uint32_t pb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((kp + 1) << 2), (int)dv);
-            const uint32_t ps = 8 * (pf & 3);
-            const uint32_t pv = ps ? (pa << ps) | (pb >> (32 - ps)) : pa;
-            const uint32_t y = (pv ^ BE32_LANES16(cand)) & (uint32_t)(((int32_t)(lane - 16)) >> 31);
+            const uint32_t y = (PV_LANES16(pf) ^ BE32_LANES16(cand)) & (uint32_t)(((int32_t)(lane - 16)) >> 31);
             const uint64_t bad = __ballot(y != 0);
 #ifdef SNAPPY_K1R_MSTAMPS
             MSTAMP(m1);
@@ -731,6 +737,7 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
         SEG(4, s4, s5);
     }
 #undef WINDOW_AT
+#undef PV_LANES16
 #undef TAG_OF
 #undef TBL_READ
 #undef TBL_WRITE

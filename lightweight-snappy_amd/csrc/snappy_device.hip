@@ -194,7 +194,7 @@ static int compress_impl(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t
     }
     const size_t units = (n + unit - 1) / unit;
     int rc;
-    if (unit <= SNAPPY_K1R_MAX_UNIT && !getenv("SNAPPY_AMD_FORCE_LDS_K1")) {
+    if (!getenv("SNAPPY_AMD_FORCE_LDS_K1")) {
         // register-resident match finder -> tokens; scan; emit in place
         const uint32_t tok_cap = unit / 4 + 2;
         if ((rc = grow(reinterpret_cast<void **>(&c->tokens), &c->tokens_cap,
@@ -204,9 +204,15 @@ static int compress_impl(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t
         if ((rc = grow(reinterpret_cast<void **>(&c->sizes), &c->sizes_cap, units * sizeof(uint32_t)))) return rc;
         const uint32_t hm = hdr_mode_of(layout, flags);
         if (c->timing) (void)hipEventRecord(c->ev[0], c->stream);
-        hipLaunchKernelGGL(k1r_match_units, dim3((uint32_t)units), dim3(64), 0, c->stream,
-                           static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens, tok_cap,
-                           c->ntok, c->sizes);
+        // units <= 32 KiB: unit in VGPRs (3 waves/SIMD); 64 KiB blocks: VGPRs + AGPRs (1 wave/SIMD)
+        if (unit <= SNAPPY_K1R_MAX_UNIT)
+            hipLaunchKernelGGL(k1r_match_units, dim3((uint32_t)units), dim3(64), 0, c->stream,
+                               static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens,
+                               tok_cap, c->ntok, c->sizes);
+        else
+            hipLaunchKernelGGL(k1r_match_units64, dim3((uint32_t)units), dim3(64), 0, c->stream,
+                               static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens,
+                               tok_cap, c->ntok, c->sizes);
         HIP_OK(hipGetLastError());
         if (c->timing) (void)hipEventRecord(c->ev[1], c->stream);
         hipLaunchKernelGGL(k2s_size_units, dim3((uint32_t)units), dim3(64), 0, c->stream, (uint64_t)n, unit, hm,

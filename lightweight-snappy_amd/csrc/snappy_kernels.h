@@ -37,6 +37,9 @@ __global__ void k1_compress_units(const uint8_t *__restrict__ in, uint64_t n, ui
 __global__ void k1r_match_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit, uint32_t hdr_mode,
                                 uint64_t header_value, uint2 *__restrict__ tokens, uint32_t tok_cap,
                                 uint32_t *__restrict__ ntok_out, uint32_t *__restrict__ sizes);
+__global__ void k1r_match_units64(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit, uint32_t hdr_mode,
+                                uint64_t header_value, uint2 *__restrict__ tokens, uint32_t tok_cap,
+                                uint32_t *__restrict__ ntok_out, uint32_t *__restrict__ sizes);
 __global__ void k2s_size_units(uint64_t n, uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
                                const uint2 *__restrict__ tokens, uint32_t tok_cap, const uint32_t *__restrict__ ntok,
                                uint32_t *__restrict__ sizes);

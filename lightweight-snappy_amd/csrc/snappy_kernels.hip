@@ -321,14 +321,17 @@ __global__ __launch_bounds__(64) void k1_compress_units(const uint8_t *__restric
 // ---------------------------------------------------------------------------
 typedef uint32_t v32 __attribute__((ext_vector_type(32)));
 typedef uint32_t v12u __attribute__((ext_vector_type(12)));
+typedef uint32_t v8u __attribute__((ext_vector_type(8)));
 
 constexpr uint32_t kTagMul = 0x9E3779B1u;
-constexpr uint32_t kRegs = 140;  // VGPRs holding the unit (60 dwords each): dwords < 8400
+constexpr uint32_t kRegs = 140;     // VGPRs holding a unit (60 dwords each): dwords < 8400 (32 KiB units)
+constexpr uint32_t kRegsBig = 276;  // 65,536-byte units: 140 VGPRs + 136 AGPRs
 
-// VGPR v[2 + r] of the resident unit (r wave-uniform).  g0..g4 are pinned
-// to v2..v141 by the constraints, so the relative move is exact whatever
-// else the allocator does.
-#define REG_OF(r)                                                                                   \
+// Register r (wave-uniform) of the resident unit.  g0..g4 are pinned to
+// v2..v141 and ag0..ag4 (65,536-byte units only) to a0..a135 by the asm
+// constraints, so the relative move (s_set_gpr_idx_on, SRC0) is exact
+// whatever else the allocator does; AGPRs are read with v_accvgpr_read.
+#define REG_OF_V(r)                                                                                 \
     ({                                                                                              \
         uint32_t _v;                                                                                \
         asm volatile("s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\tv_mov_b32 %0, v2\n\ts_set_gpr_idx_off"      \
@@ -337,8 +340,31 @@ constexpr uint32_t kRegs = 140;  // VGPRs holding the unit (60 dwords each): dwo
                        "{v[98:129]}"(g3), "{v[130:141]}"(g4));                                      \
         _v;                                                                                         \
     })
+// AGPRs a0..a135 are written once by the prologue's v_accvgpr_write asm
+// (with the registers as clobbers, so the kernel allocates them) and are
+// otherwise invisible to the compiler, which never needs AGPRs here
+#define REG_OF_A(r)                                                                                 \
+    ({                                                                                              \
+        uint32_t _v;                                                                                \
+        asm volatile("s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\tv_accvgpr_read_b32 %0, a0\n\ts_set_gpr_idx_off" \
+                     : "=&v"(_v)                                                                    \
+                     : "s"((uint32_t)(r)));                                                         \
+        _v;                                                                                         \
+    })
+#define REG_OF(r)                                                                                   \
+    ({                                                                                              \
+        const uint32_t _rr = (r);                                                                   \
+        uint32_t _rv;                                                                               \
+        if constexpr (BIG) {                                                                        \
+            if (_rr < kRegs) _rv = REG_OF_V(_rr);                                                   \
+            else _rv = REG_OF_A(_rr - kRegs);                                                       \
+        } else {                                                                                    \
+            _rv = REG_OF_V(_rr);                                                                    \
+        }                                                                                           \
+        _rv;                                                                                        \
+    })
 
-// halo layout: dword d -> VGPR d / 60, lane d % 60 (exact for d < 8400)
+// halo layout: dword d -> register d / 60, lane d % 60 (exact for d < 16600)
 #define HALO_R(d) (((d) * 17477u) >> 20)
 
 // BE32 load at byte q (src/snappy_compression.c:239-241), q wave-uniform
@@ -365,9 +391,9 @@ constexpr uint32_t kRegs = 140;  // VGPRs holding the unit (60 dwords each): dwo
         const uint32_t _le = _e - 60 * (_R + _re);                                                     \
         const uint32_t _x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)REG_OF(_R));  \
         const uint32_t _x1 = (uint32_t)__builtin_amdgcn_ds_bpermute(                                   \
-            (int)(_le << 2), (int)(_R + 1 < kRegs ? REG_OF(_R + 1) : 0));                              \
+            (int)(_le << 2), (int)(_R + 1 < NREG ? REG_OF(_R + 1) : 0));                               \
         const uint32_t _x2 = (uint32_t)__builtin_amdgcn_ds_bpermute(                                   \
-            (int)(_le << 2), (int)(_R + 2 < kRegs ? REG_OF(_R + 2) : 0));                              \
+            (int)(_le << 2), (int)(_R + 2 < NREG ? REG_OF(_R + 2) : 0));                               \
         _re == 0 ? _x0 : (_re == 1 ? _x1 : _x2);                                                       \
     })
 
@@ -488,13 +514,15 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
 #define SEG(i, a, b) do { } while (0)
 #endif
 
-__global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
-                                                          uint32_t hdr_mode, uint64_t header_value,
-                                                          uint2 *__restrict__ tokens, uint32_t tok_cap,
-                                                          uint32_t *__restrict__ ntok_out,
-                                                          uint32_t *__restrict__ sizes)
+template <bool BIG>
+__device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit, uint32_t hdr_mode,
+                                         uint64_t header_value, uint2 *__restrict__ tokens, uint32_t tok_cap,
+                                         uint32_t *__restrict__ ntok_out, uint32_t *__restrict__ sizes)
 {
     constexpr int W = SNAPPY_K1R_WINDOW;
+    constexpr uint32_t NREG = BIG ? kRegsBig : kRegs;
+    (void)hdr_mode;
+    (void)header_value;
 #ifndef SNAPPY_K1R_TABLE16
     // 12 KiB: u16 positions + u8 tags: 12 units/CU (the VGPR limit) instead of
     // 10 with u32 entries
@@ -523,9 +551,9 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
     v32 g0, g1, g2, g3;
     v12u g4;
     const bool aligned = ((reinterpret_cast<uintptr_t>(src) & 3) == 0);
-#pragma unroll
-    for (int i = 0; i < (int)kRegs; i++) {
-        const uint32_t d = 60 * i + lane;  // lanes 60..63: the next VGPR's first dwords
+    // big-endian dword (halo layout) of register i, zero past the end
+    auto load_word = [&](uint32_t i) -> uint32_t {
+        const uint32_t d = 60 * i + lane;  // lanes 60..63: the next register's first dwords
         const uint32_t b = 4 * d;
         uint32_t w = 0;
         if (b + 4 <= L && aligned) {
@@ -534,12 +562,156 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
             for (uint32_t k = 0; k < 4; k++)
                 if (b + k < L) w |= (uint32_t)src[b + k] << (8 * k);
         }
-        w = __builtin_bswap32(w);
+        return __builtin_bswap32(w);
+    };
+#pragma unroll
+    for (int i = 0; i < (int)kRegs; i++) {
+        const uint32_t w = load_word(i);
         if (i < 32) g0[i] = w;
         else if (i < 64) g1[i - 32] = w;
         else if (i < 96) g2[i - 64] = w;
         else if (i < 128) g3[i - 96] = w;
         else g4[i - 128] = w;
+    }
+    if constexpr (BIG) {
+#define K1R_AW(k) asm volatile("v_accvgpr_write_b32 a" #k ", %0" ::"v"(load_word(kRegs + (k))) : "a" #k)
+        K1R_AW(0);
+        K1R_AW(1);
+        K1R_AW(2);
+        K1R_AW(3);
+        K1R_AW(4);
+        K1R_AW(5);
+        K1R_AW(6);
+        K1R_AW(7);
+        K1R_AW(8);
+        K1R_AW(9);
+        K1R_AW(10);
+        K1R_AW(11);
+        K1R_AW(12);
+        K1R_AW(13);
+        K1R_AW(14);
+        K1R_AW(15);
+        K1R_AW(16);
+        K1R_AW(17);
+        K1R_AW(18);
+        K1R_AW(19);
+        K1R_AW(20);
+        K1R_AW(21);
+        K1R_AW(22);
+        K1R_AW(23);
+        K1R_AW(24);
+        K1R_AW(25);
+        K1R_AW(26);
+        K1R_AW(27);
+        K1R_AW(28);
+        K1R_AW(29);
+        K1R_AW(30);
+        K1R_AW(31);
+        K1R_AW(32);
+        K1R_AW(33);
+        K1R_AW(34);
+        K1R_AW(35);
+        K1R_AW(36);
+        K1R_AW(37);
+        K1R_AW(38);
+        K1R_AW(39);
+        K1R_AW(40);
+        K1R_AW(41);
+        K1R_AW(42);
+        K1R_AW(43);
+        K1R_AW(44);
+        K1R_AW(45);
+        K1R_AW(46);
+        K1R_AW(47);
+        K1R_AW(48);
+        K1R_AW(49);
+        K1R_AW(50);
+        K1R_AW(51);
+        K1R_AW(52);
+        K1R_AW(53);
+        K1R_AW(54);
+        K1R_AW(55);
+        K1R_AW(56);
+        K1R_AW(57);
+        K1R_AW(58);
+        K1R_AW(59);
+        K1R_AW(60);
+        K1R_AW(61);
+        K1R_AW(62);
+        K1R_AW(63);
+        K1R_AW(64);
+        K1R_AW(65);
+        K1R_AW(66);
+        K1R_AW(67);
+        K1R_AW(68);
+        K1R_AW(69);
+        K1R_AW(70);
+        K1R_AW(71);
+        K1R_AW(72);
+        K1R_AW(73);
+        K1R_AW(74);
+        K1R_AW(75);
+        K1R_AW(76);
+        K1R_AW(77);
+        K1R_AW(78);
+        K1R_AW(79);
+        K1R_AW(80);
+        K1R_AW(81);
+        K1R_AW(82);
+        K1R_AW(83);
+        K1R_AW(84);
+        K1R_AW(85);
+        K1R_AW(86);
+        K1R_AW(87);
+        K1R_AW(88);
+        K1R_AW(89);
+        K1R_AW(90);
+        K1R_AW(91);
+        K1R_AW(92);
+        K1R_AW(93);
+        K1R_AW(94);
+        K1R_AW(95);
+        K1R_AW(96);
+        K1R_AW(97);
+        K1R_AW(98);
+        K1R_AW(99);
+        K1R_AW(100);
+        K1R_AW(101);
+        K1R_AW(102);
+        K1R_AW(103);
+        K1R_AW(104);
+        K1R_AW(105);
+        K1R_AW(106);
+        K1R_AW(107);
+        K1R_AW(108);
+        K1R_AW(109);
+        K1R_AW(110);
+        K1R_AW(111);
+        K1R_AW(112);
+        K1R_AW(113);
+        K1R_AW(114);
+        K1R_AW(115);
+        K1R_AW(116);
+        K1R_AW(117);
+        K1R_AW(118);
+        K1R_AW(119);
+        K1R_AW(120);
+        K1R_AW(121);
+        K1R_AW(122);
+        K1R_AW(123);
+        K1R_AW(124);
+        K1R_AW(125);
+        K1R_AW(126);
+        K1R_AW(127);
+        K1R_AW(128);
+        K1R_AW(129);
+        K1R_AW(130);
+        K1R_AW(131);
+        K1R_AW(132);
+        K1R_AW(133);
+        K1R_AW(134);
+        K1R_AW(135);
+#undef K1R_AW
     }
 
     uint32_t T = 256, lg = 8;  // set_htable_size :198-204
@@ -760,6 +932,26 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
 #endif
     }
 #endif
+}
+
+__global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
+                                                          uint32_t hdr_mode, uint64_t header_value,
+                                                          uint2 *__restrict__ tokens, uint32_t tok_cap,
+                                                          uint32_t *__restrict__ ntok_out,
+                                                          uint32_t *__restrict__ sizes)
+{
+    k1r_body<false>(in, n, unit, hdr_mode, header_value, tokens, tok_cap, ntok_out, sizes);
+}
+
+// 65,536-byte blocks (the reference's MAX_BLOCK_SIZE): unit in 140 VGPRs +
+// 136 AGPRs, one wave per SIMD
+__global__ __launch_bounds__(64, 1) void k1r_match_units64(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
+                                                            uint32_t hdr_mode, uint64_t header_value,
+                                                            uint2 *__restrict__ tokens, uint32_t tok_cap,
+                                                            uint32_t *__restrict__ ntok_out,
+                                                            uint32_t *__restrict__ sizes)
+{
+    k1r_body<true>(in, n, unit, hdr_mode, header_value, tokens, tok_cap, ntok_out, sizes);
 }
 
 // ---------------------------------------------------------------------------

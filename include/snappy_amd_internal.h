@@ -8,6 +8,7 @@
 #define SNAPPY_AMD_INTERNAL_H
 #include <stddef.h>
 #include <stdint.h>
+#include <stdio.h>
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -17,6 +18,10 @@ extern "C" {
 int snappy_amd_host_compress(const uint8_t *in, size_t n, uint64_t header_value, uint8_t *out, size_t cap,
                              size_t *out_len);
 int snappy_amd_host_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len);
+/* Streaming form of snappy_compress(): reads fin from its current position
+ * to EOF in 64 MiB chunks, writes the same bytes as the whole-input call
+ * (varint(header_value) ++ blocks) to fout; *bytes_in = bytes read. */
+int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, uint64_t *bytes_in);
 #ifdef __cplusplus
 }
 #endif

@@ -4,6 +4,7 @@
 // include/snappy_amd_internal.h (host-buffer helpers used by snappy_host.c).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <mutex>
@@ -419,6 +420,107 @@ int snappy_amd_host_compress(const uint8_t *in, size_t n, uint64_t header_value,
     HIP_OK(hipMemcpyAsync(out, c->d_b, len, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
     *out_len = len;
+    return SNAPPY_AMD_OK;
+}
+
+// Streaming FILE* compress: the reference's fread/compress/
+// fwrite block loop (snappy_compression.c:419-425) as a two-slot pipeline of
+// 64 MiB chunks (a multiple of the 65,536-byte block, so block boundaries and
+// bytes are those of the whole-input stream).  Slot k%2 has its own context
+// (stream), pinned staging and device buffers: while chunk k's H2D + kernels
+// run, the host writes chunk k-1 (exact-size D2H on the other stream) and
+// reads chunk k+1.  Chunk 0 carries the varint(header_value) preamble, the
+// others are compressed with it suppressed.
+namespace {
+struct StreamSlot {
+    snappy_amd_ctx *c = nullptr;
+    uint8_t *h_in = nullptr, *h_out = nullptr;
+    uint8_t *d_in = nullptr, *d_out = nullptr;
+    uint64_t *d_idx = nullptr;
+    size_t n = 0;
+    bool busy = false;
+};
+constexpr size_t kStreamChunk = (size_t)64 << 20;
+StreamSlot g_slots[2];
+
+size_t read_full(FILE *f, uint8_t *b, size_t cap)
+{
+    size_t n = 0;
+    while (n < cap) {
+        const size_t got = fread(b + n, 1, cap - n, f);
+        if (got == 0) break;
+        n += got;
+    }
+    return n;
+}
+
+int slot_init(StreamSlot &s, int device)
+{
+    if (s.c) return SNAPPY_AMD_OK;
+    int rc = snappy_amd_create(device, &s.c);
+    if (rc) return rc;
+    const size_t maxo = snappy_amd_max_output(kStreamChunk, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE);
+    const size_t units = kStreamChunk / SNAPPY_AMD_BLOCK;
+    if (hipHostMalloc(&s.h_in, kStreamChunk, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&s.h_out, maxo, hipHostMallocDefault) != hipSuccess ||
+        hipMalloc(&s.d_in, kStreamChunk) != hipSuccess || hipMalloc(&s.d_out, maxo) != hipSuccess ||
+        hipMalloc(&s.d_idx, (units + 1) * sizeof(uint64_t)) != hipSuccess)
+        return SNAPPY_AMD_ERR_DEVICE;
+    return SNAPPY_AMD_OK;
+}
+
+// finish slot s: its compressed size is in s.c->h_total once its stream drains
+int slot_drain(StreamSlot &s, FILE *fout)
+{
+    if (!s.busy) return SNAPPY_AMD_OK;
+    s.busy = false;
+    HIP_OK(hipStreamSynchronize(s.c->stream));
+    const size_t len = (size_t)*s.c->h_total;
+    HIP_OK(hipMemcpyAsync(s.h_out, s.d_out, len, hipMemcpyDeviceToHost, s.c->stream));
+    HIP_OK(hipStreamSynchronize(s.c->stream));
+    if (len && fwrite(s.h_out, 1, len, fout) != len) return SNAPPY_AMD_ERR_IO;
+    return SNAPPY_AMD_OK;
+}
+}  // namespace
+
+int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, uint64_t *bytes_in)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!fin || !fout) return SNAPPY_AMD_ERR_ARG;
+    int dev = 0;
+    if (const char *e = getenv("SNAPPY_AMD_DEVICE")) dev = atoi(e);
+    int rc;
+    for (auto &s : g_slots) {
+        if ((rc = slot_init(s, dev))) return rc;
+        if (s.busy) {  // left over by a failed call: discard
+            (void)hipStreamSynchronize(s.c->stream);
+            s.busy = false;
+        }
+    }
+    HIP_OK(hipSetDevice(dev));
+    uint64_t total_in = 0;
+    size_t n = read_full(fin, g_slots[0].h_in, kStreamChunk);
+    if (ferror(fin)) return SNAPPY_AMD_ERR_IO;
+    for (uint32_t k = 0; n > 0; k++) {
+        StreamSlot &s = g_slots[k & 1];
+        StreamSlot &o = g_slots[(k + 1) & 1];
+        s.n = n;
+        total_in += n;
+        HIP_OK(hipMemcpyAsync(s.d_in, s.h_in, n, hipMemcpyHostToDevice, s.c->stream));
+        rc = compress_impl(s.c, s.d_in, n, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE, k ? SNAPPY_AMD_NO_PREAMBLE : 0,
+                           header_value, s.d_out, s.d_idx, nullptr);
+        if (rc) return rc;
+        HIP_OK(hipMemcpyAsync(s.c->h_total, s.c->total, sizeof(uint64_t), hipMemcpyDeviceToHost, s.c->stream));
+        s.busy = true;
+        // chunk k-1 out while chunk k runs, then chunk k+1 in (its slot is free
+        // once chunk k-1 drained)
+        if ((rc = slot_drain(o, fout))) return rc;
+        n = read_full(fin, o.h_in, kStreamChunk);
+        if (ferror(fin)) return SNAPPY_AMD_ERR_IO;
+    }
+    for (auto &s : g_slots)
+        if ((rc = slot_drain(s, fout))) return rc;
+    if (bytes_in) *bytes_in = total_in;
     return SNAPPY_AMD_OK;
 }
 

@@ -94,18 +94,11 @@ static int slurp(FILE *f, uint8_t **buf, size_t *len)
 
 void snappy_compress(FILE *file_input, unsigned long long input_size, FILE *file_compressed)
 {
-    uint8_t *in = NULL, *out = NULL;
-    size_t n = 0, len = 0;
-    int rc = (file_input && file_compressed) ? slurp(file_input, &in, &n) : SNAPPY_AMD_ERR_ARG;
-    if (rc == SNAPPY_AMD_OK && n > 0) {
-        /* header = the caller's input_size, as the reference writes it */
-        size_t cap = snappy_max_compressed_length(n);
-        out = (uint8_t *)malloc(cap);
-        rc = out ? snappy_amd_host_compress(in, n, (uint64_t)input_size, out, cap, &len) : SNAPPY_AMD_ERR_IO;
-        if (rc == SNAPPY_AMD_OK && fwrite(out, 1, len, file_compressed) != len) rc = SNAPPY_AMD_ERR_IO;
-    }
-    free(in);
-    free(out);
+    /* header = the caller's input_size, as the reference writes it; an empty
+     * read writes nothing (snappy_compression.c:417-421) */
+    int rc = (file_input && file_compressed)
+                 ? snappy_amd_host_compress_file(file_input, (uint64_t)input_size, file_compressed, NULL)
+                 : SNAPPY_AMD_ERR_ARG;
     g_last_status = rc;
     if (rc != SNAPPY_AMD_OK) fprintf(stderr, "snappy_compress: error %d\n", rc);
 }

@@ -92,6 +92,8 @@ _SIGS = {
                                             _c.POINTER(_c.c_size_t)]),
     "snappy_amd_host_decompress": (_c.c_int, [_c.c_void_p, _c.c_size_t, _c.c_void_p, _c.c_size_t,
                                               _c.POINTER(_c.c_size_t)]),
+    # FILE* in, header value, FILE* out, bytes read (C stdio streams; used by the C host layer)
+    "snappy_amd_host_compress_file": (_c.c_int, [_c.c_void_p, _c.c_uint64, _c.c_void_p, _c.POINTER(_c.c_uint64)]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -140,6 +140,24 @@ def test_cli_round_trip(golden):
         assert r.returncode != 0
 
 
+def test_cli_streaming_multi_chunk():
+    """snappy_compress(FILE*) streams 64 MiB chunks through two pipeline slots:
+    a 150 MiB mixed input (text, random, zeros; not a multiple of 65,536) must
+    come out byte-identical to the one-shot reference stream."""
+    exe = os.path.join(ROOT, "lightweight-snappy_amd", "snappy")
+    data = np.concatenate([datagen.make("T", 70 << 20, 41), datagen.make("R", 30 << 20, 42),
+                           np.zeros(10 << 20, np.uint8), datagen.make("T", (40 << 20) + 12345, 43)]).tobytes()
+    want = oracle.compress(data)
+    with tempfile.TemporaryDirectory() as d:
+        src, snp, dec = (os.path.join(d, x) for x in ("in", "in.snp", "in.dec"))
+        open(src, "wb").write(data)
+        subprocess.run([exe, "-c", src, snp], check=True, capture_output=True)
+        got = open(snp, "rb").read()
+        assert len(got) == len(want) and got == want
+        subprocess.run([exe, "-d", snp, dec], check=True, capture_output=True)
+        assert open(dec, "rb").read() == data
+
+
 def test_full_size_streams_1gib(codec):
     """BASELINE.json configs[1] at full size: 1 GiB of 32 KiB text streams,
     bit-exact against the (threaded) oracle and round-tripped on the GPU."""

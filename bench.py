@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--assemble", action="store_true", help="also time the RCCL all-gather of shards")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-e2e", action="store_true", help="skip the PCIe-inclusive host API sample")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="nccl (= RCCL, the real path) or gloo (CPU collectives; rehearsal with ranks sharing a GPU)")
     ap.add_argument("--cpu-sample-bytes", type=int, default=1 << 30)
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="rocprofv3 PMC summary giving HBM traffic per launch (see profiles/README.md)")
@@ -164,13 +166,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gloo = args.dist_backend == "gloo"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # gloo: rehearsal of the multi-rank path (ranks may share a GPU)
+        local = local % torch.cuda.device_count() if gloo else local
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
+    cdev = torch.device("cpu") if gloo else dev  # where collective tensors live
 
     kind, seed, layout, chunk, desc = WORKLOADS[args.workload]
     n = args.bytes_per_gpu
@@ -188,14 +197,23 @@ def main():
     # SINGLE layout sharded over ranks: rank 0 carries the global preamble
     flags = snappy_amd.NO_PREAMBLE if (layout == snappy_amd.SINGLE and rank > 0) else 0
     header_value = n * world if layout == snappy_amd.SINGLE else n
-    sizes_t = torch.zeros(world, dtype=torch.int64, device=dev)
+    sizes_t = torch.zeros(world, dtype=torch.int64, device=cdev)
+
+    def allgather(dst, src):
+        if gloo:
+            parts = list(dst.chunk(world))
+            dist.all_gather(parts, src)
+            if parts[0].data_ptr() != dst.data_ptr():
+                dst.copy_(torch.cat(parts))
+        else:
+            dist.all_gather_into_tensor(dst, src)
 
     def step():
         clen = codec.compress_ptr_ex(x.data_ptr(), n, chunk, layout, flags, header_value, out.data_ptr(),
                                      offs.data_ptr())
         if world > 1:  # C1: shard sizes -> global stream offsets
-            mine = torch.tensor([clen], dtype=torch.int64, device=dev)
-            dist.all_gather_into_tensor(sizes_t, mine)
+            mine = torch.tensor([clen], dtype=torch.int64, device=cdev)
+            allgather(sizes_t, mine)
         codec.decompress_ptr_ex(out.data_ptr(), offs.data_ptr(), n, chunk, layout, flags, header_value,
                                 back.data_ptr(), check=False)
         return clen
@@ -221,11 +239,11 @@ def main():
     st = codec.decompress_status()
     ok = st == 0 and bool(torch.equal(back, x))
     if world > 1:
-        t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, bad = float(t[0]), float(t[1])
         ok = bad == 0.0
-        tot = torch.tensor([clen], dtype=torch.int64, device=dev)
+        tot = torch.tensor([clen], dtype=torch.int64, device=cdev)
         dist.all_reduce(tot)
         total_comp = int(tot)
     else:
@@ -237,10 +255,10 @@ def main():
         dist.barrier()
         ta = time.perf_counter()
         mx = int(sizes_t.max())
-        pad = torch.zeros(mx, dtype=torch.uint8, device=dev)
-        pad[:clen] = out[:clen]
-        full = torch.empty(world * mx, dtype=torch.uint8, device=dev)
-        dist.all_gather_into_tensor(full, pad)
+        pad = torch.zeros(mx, dtype=torch.uint8, device=cdev)
+        pad[:clen] = out[:clen].to(cdev)
+        full = torch.empty(world * mx, dtype=torch.uint8, device=cdev)
+        allgather(full, pad)
         torch.cuda.synchronize(dev)
         dist.barrier()
         tb = time.perf_counter() - ta
@@ -255,7 +273,9 @@ def main():
     comp_bytes = clen  # this rank's compressed output
     # dominant kernel (longest average launch) and its algorithmic bytes per
     # launch: compress = N_in + N_out, decompress = N_comp + N_out
-    k1_name = "k1r_match_units" if chunk <= 32768 else "k1_compress_units"
+    k1_name = "k1r_match_units" if chunk <= 32768 else "k1r_match_units64"
+    if os.environ.get("SNAPPY_AMD_FORCE_LDS_K1"):
+        k1_name = "k1_compress_units"
     cands = [(k1m, k1_name, n + comp_bytes), (k4m, "k4_decompress_units", comp_bytes + n)]
     dom_ms, dom_name, dom_bytes = max(cands)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
@@ -277,7 +297,7 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": f"{args.workload}: {desc}; one step = compress + decompress round trip",
+            "config": {"workload": f"{args.workload}: {desc.replace('1 GiB/GPU', f'{n / 2**30:g} GiB/GPU')}; one step = compress + decompress round trip",
                        "bytes_per_gpu": n, "chunk": chunk, "layout": "STREAMS" if layout else "SINGLE",
                        "units_per_gpu": units, "parallelism": f"dp{world} (block shards)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -298,11 +298,11 @@ __global__ __launch_bounds__(64) void k1_compress_units(const uint8_t *__restric
 // K1r: register-resident match finder for units <= 32 KiB (the STREAMS
 // layout of BASELINE.json configs[1]).
 //
-//  * The unit lives in 140 VGPRs of its wave (v2..v141), "halo" layout:
-//    VGPR r, lane l < 60 holds big-endian dword 60 r + l and lanes 60..63
-//    repeat the next VGPR's first four dwords, so any 4 consecutive dwords
-//    sit in one VGPR: a wave-uniform unaligned load of up to 12 bytes is one
-//    s_set_gpr_idx + v_mov + v_readlanes, with no branches.
+//  * The unit lives in 131 VGPRs of its wave (v2..v132), "halo" layout:
+//    VGPR r, lane l < 63 holds big-endian dword 63 r + l and lane 63 repeats
+//    the next VGPR's first dword, so any 2 consecutive dwords sit in one
+//    VGPR (a wave-uniform unaligned BE32 is one s_set_gpr_idx + v_mov +
+//    v_readlanes) and any 64 consecutive dwords span two VGPRs.
 //  * The hash table is u32 in LDS (16 KiB): position (low 16 bits) and a
 //    16-bit tag of the 4 bytes there (high 16 bits).  A probe whose tag
 //    differs is a miss decided without touching the input; equal tags are
@@ -320,27 +320,27 @@ __global__ __launch_bounds__(64) void k1_compress_units(const uint8_t *__restric
 // VGPR budget <= 168 -> 3 waves per SIMD; LDS 16 KiB -> 10 units per CU.
 // ---------------------------------------------------------------------------
 typedef uint32_t v32 __attribute__((ext_vector_type(32)));
-typedef uint32_t v12u __attribute__((ext_vector_type(12)));
+typedef uint32_t v3u __attribute__((ext_vector_type(3)));
 typedef uint32_t v8u __attribute__((ext_vector_type(8)));
 
 constexpr uint32_t kTagMul = 0x9E3779B1u;
-constexpr uint32_t kRegs = 140;     // VGPRs holding a unit (60 dwords each): dwords < 8400 (32 KiB units)
-constexpr uint32_t kRegsBig = 276;  // 65,536-byte units: 140 VGPRs + 136 AGPRs
+constexpr uint32_t kRegs = 131;     // VGPRs holding a unit (63 dwords each): dwords < 8253 (32 KiB units)
+constexpr uint32_t kRegsBig = 261;  // 65,536-byte units: 131 VGPRs + 130 AGPRs
 
 // Register r (wave-uniform) of the resident unit.  g0..g4 are pinned to
-// v2..v141 and ag0..ag4 (65,536-byte units only) to a0..a135 by the asm
-// constraints, so the relative move (s_set_gpr_idx_on, SRC0) is exact
-// whatever else the allocator does; AGPRs are read with v_accvgpr_read.
+// v2..v132 by the asm constraints (65,536-byte units continue in a0..a129),
+// so the relative move (s_set_gpr_idx_on, SRC0) is exact whatever else the
+// allocator does; AGPRs are read with v_accvgpr_read.
 #define REG_OF_V(r)                                                                                 \
     ({                                                                                              \
         uint32_t _v;                                                                                \
         asm volatile("s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\tv_mov_b32 %0, v2\n\ts_set_gpr_idx_off"      \
                      : "=&v"(_v)                                                                    \
                      : "s"((uint32_t)(r)), "{v[2:33]}"(g0), "{v[34:65]}"(g1), "{v[66:97]}"(g2),          \
-                       "{v[98:129]}"(g3), "{v[130:141]}"(g4));                                      \
+                       "{v[98:129]}"(g3), "{v[130:132]}"(g4));                                      \
         _v;                                                                                         \
     })
-// AGPRs a0..a135 are written once by the prologue's v_accvgpr_write asm
+// AGPRs a0..a129 are written once by the prologue's v_accvgpr_write asm
 // (with the registers as clobbers, so the kernel allocates them) and are
 // otherwise invisible to the compiler, which never needs AGPRs here
 #define REG_OF_A(r)                                                                                 \
@@ -364,8 +364,8 @@ constexpr uint32_t kRegsBig = 276;  // 65,536-byte units: 140 VGPRs + 136 AGPRs
         _rv;                                                                                        \
     })
 
-// halo layout: dword d -> register d / 60, lane d % 60 (exact for d < 16600)
-#define HALO_R(d) (((d) * 17477u) >> 20)
+// halo layout: dword d -> register d / 63, lane d % 63 (exact for d < 16700)
+#define HALO_R(d) (((d) * 16645u) >> 20)
 
 // BE32 load at byte q (src/snappy_compression.c:239-241), q wave-uniform
 #define BE32_REG(qq)                                                        \
@@ -373,28 +373,26 @@ constexpr uint32_t kRegsBig = 276;  // 65,536-byte units: 140 VGPRs + 136 AGPRs
         const uint32_t _q = (qq);                                           \
         const uint32_t _d = _q >> 2;                                        \
         const uint32_t _r = HALO_R(_d);                                     \
-        const uint32_t _l = _d - 60 * _r;                                   \
+        const uint32_t _l = _d - 63 * _r;                                   \
         const uint32_t _v = REG_OF(_r);                                     \
         const uint32_t _hi = __builtin_amdgcn_readlane(_v, _l);             \
         const uint32_t _lo = __builtin_amdgcn_readlane(_v, _l + 1);         \
         (uint32_t)(((((uint64_t)_hi) << 32 | _lo) << (8 * (_q & 3))) >> 32); \
     })
 
-// per-lane dword e = d0 + lane (d0 uniform): the 64 dwords span at most
-// VGPRs R..R+2 of the halo layout
+// per-lane dword e = d0 + lane (d0 uniform): the 64 dwords span VGPRs R, R+1
+// of the halo layout
 #define DW_LANES(dd0)                                                                                  \
     ({                                                                                                 \
         const uint32_t _d0 = (dd0);                                                                    \
         const uint32_t _R = HALO_R(_d0);                                                               \
         const uint32_t _e = _d0 + lane;                                                                \
-        const uint32_t _re = HALO_R(_e) - _R; /* 0..2 */                                              \
-        const uint32_t _le = _e - 60 * (_R + _re);                                                     \
+        const uint32_t _re = HALO_R(_e) - _R; /* 0..1 */                                              \
+        const uint32_t _le = _e - 63 * (_R + _re);                                                     \
         const uint32_t _x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)REG_OF(_R));  \
         const uint32_t _x1 = (uint32_t)__builtin_amdgcn_ds_bpermute(                                   \
             (int)(_le << 2), (int)(_R + 1 < NREG ? REG_OF(_R + 1) : 0));                               \
-        const uint32_t _x2 = (uint32_t)__builtin_amdgcn_ds_bpermute(                                   \
-            (int)(_le << 2), (int)(_R + 2 < NREG ? REG_OF(_R + 2) : 0));                               \
-        _re == 0 ? _x0 : (_re == 1 ? _x1 : _x2);                                                       \
+        _re == 0 ? _x0 : _x1;                                                                          \
     })
 
 __device__ __forceinline__ uint32_t varint_len(uint64_t v)
@@ -481,8 +479,8 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
         const uint32_t _R = HALO_R(_d0);                                                             \
         const uint32_t _e = _d0 + (lane & 15);                                                       \
         const uint32_t _re = HALO_R(_e) - _R; /* 0..1 */                                            \
-        const uint32_t _le = _e - 60 * (_R + _re);                                                   \
-        const uint32_t _r0 = REG_OF(_R), _r1 = REG_OF(_R + 1);                                      \
+        const uint32_t _le = _e - 63 * (_R + _re);                                                   \
+        const uint32_t _r0 = REG_OF(_R), _r1 = _R + 1 < NREG ? REG_OF(_R + 1) : 0;                  \
         const uint32_t _x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)_r0);      \
         const uint32_t _x1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_le + 1) << 2), (int)_r0);\
         const uint32_t _y0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)_r1);      \
@@ -549,11 +547,11 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 
     // unit -> VGPRs (halo layout), big-endian, zero past the end
     v32 g0, g1, g2, g3;
-    v12u g4;
+    v3u g4;
     const bool aligned = ((reinterpret_cast<uintptr_t>(src) & 3) == 0);
     // big-endian dword (halo layout) of register i, zero past the end
     auto load_word = [&](uint32_t i) -> uint32_t {
-        const uint32_t d = 60 * i + lane;  // lanes 60..63: the next register's first dwords
+        const uint32_t d = 63 * i + lane;  // lane 63: the next register's first dword
         const uint32_t b = 4 * d;
         uint32_t w = 0;
         if (b + 4 <= L && aligned) {
@@ -705,12 +703,6 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         K1R_AW(127);
         K1R_AW(128);
         K1R_AW(129);
-        K1R_AW(130);
-        K1R_AW(131);
-        K1R_AW(132);
-        K1R_AW(133);
-        K1R_AW(134);
-        K1R_AW(135);
 #undef K1R_AW
     }
 
@@ -943,8 +935,8 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
     k1r_body<false>(in, n, unit, hdr_mode, header_value, tokens, tok_cap, ntok_out, sizes);
 }
 
-// 65,536-byte blocks (the reference's MAX_BLOCK_SIZE): unit in 140 VGPRs +
-// 136 AGPRs, one wave per SIMD
+// 65,536-byte blocks (the reference's MAX_BLOCK_SIZE): unit in 131 VGPRs +
+// 130 AGPRs, one wave per SIMD
 __global__ __launch_bounds__(64, 1) void k1r_match_units64(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
                                                             uint32_t hdr_mode, uint64_t header_value,
                                                             uint2 *__restrict__ tokens, uint32_t tok_cap,

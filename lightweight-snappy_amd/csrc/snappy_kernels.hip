@@ -494,7 +494,7 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
 #define SNAPPY_K1R_WINDOW 4  // 2.6 probes per round on text: 4 speculative lanes suffice
 #endif
 
-#if defined(SNAPPY_K1R_STAMPS) || defined(SNAPPY_K1R_MSTAMPS)
+#if defined(SNAPPY_K1R_STAMPS) || defined(SNAPPY_K1R_MSTAMPS) || defined(SNAPPY_K1R_FSTAMPS)
 #define MSTAMP(var)                                                                         \
     do {                                                                                    \
         __builtin_amdgcn_sched_barrier(0);                                                  \
@@ -757,7 +757,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     uint32_t n_probe = 0, n_match = 0, n_round = 0;
     uint64_t t_match = 0;
 #endif
-#if defined(SNAPPY_K1R_STAMPS) || defined(SNAPPY_K1R_MSTAMPS)
+#if defined(SNAPPY_K1R_STAMPS) || defined(SNAPPY_K1R_MSTAMPS) || defined(SNAPPY_K1R_FSTAMPS)
     uint64_t seg[6] = {0, 0, 0, 0, 0, 0};
     uint64_t s0, s1, s2, s3, s4, s5;
 #endif
@@ -818,9 +818,12 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #ifdef SNAPPY_K1R_STATS
             const uint64_t tm0 = clock64();
 #endif
-#ifdef SNAPPY_K1R_MSTAMPS
-            uint64_t m0, m1, m2, m3;
+#if defined(SNAPPY_K1R_MSTAMPS) || defined(SNAPPY_K1R_FSTAMPS)
+            uint64_t m0;
             MSTAMP(m0);
+#endif
+#ifdef SNAPPY_K1R_MSTAMPS
+            uint64_t m1, m2, m3;
 #endif
             const uint32_t pf = __builtin_amdgcn_readlane(pk, f);
             const uint32_t cand = __builtin_amdgcn_readlane(ent, f) & 0xFFFF;
@@ -828,8 +831,40 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             // lanes 0..15 compare BE32 at pf + 4j and cand + 4j: verification
             // (first 4 bytes) and find_copy_length :61-72 up to 64 bytes at once
             // pf side from the dword window (pf <= q0 + 52 and q0 / 4 - d0 <= 34: index <= 63)
+#ifdef SNAPPY_K1R_FSTAMPS
+            // fine-grained attribution of the verification gather (stamps drain lgkm)
+            uint64_t fa, fb, fc, mf1;
+            asm volatile("" ::"s"(pf), "s"(cand), "s"(hf));
+            MSTAMP(fa);
+            const uint32_t _q = cand, _d0 = _q >> 2, _R = HALO_R(_d0);
+            const uint32_t _e = _d0 + (lane & 15);
+            const uint32_t _re = HALO_R(_e) - _R;
+            const uint32_t _le = _e - 63 * (_R + _re);
+            const uint32_t _r0 = REG_OF(_R), _r1 = _R + 1 < NREG ? REG_OF(_R + 1) : 0;
+            asm volatile("" ::"v"(_r0), "v"(_r1));
+            MSTAMP(fb);
+            const uint32_t pvv = PV_LANES16(pf);
+            const uint32_t _x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)_r0);
+            const uint32_t _x1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_le + 1) << 2), (int)_r0);
+            const uint32_t _y0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)_r1);
+            const uint32_t _y1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_le + 1) << 2), (int)_r1);
+            asm volatile("" ::"v"(_x0), "v"(_x1), "v"(_y0), "v"(_y1), "v"(pvv));
+            MSTAMP(fc);
+            const uint32_t _hi = _re ? _y0 : _x0, _lo = _re ? _y1 : _x1;
+            const uint32_t _s = 8 * (_q & 3);
+            const uint32_t cv = _s ? (_hi << _s) | (_lo >> (32 - _s)) : _hi;
+            const uint32_t y = (pvv ^ cv) & (uint32_t)(((int32_t)(lane - 16)) >> 31);
+            const uint64_t bad = __ballot(y != 0);
+            asm volatile("" ::"s"(bad));
+            MSTAMP(mf1);
+            seg[0] += fa - m0;
+            seg[1] += fb - fa;
+            seg[2] += fc - fb;
+            seg[3] += mf1 - fc;
+#else
             const uint32_t y = (PV_LANES16(pf) ^ BE32_LANES16(cand)) & (uint32_t)(((int32_t)(lane - 16)) >> 31);
             const uint64_t bad = __ballot(y != 0);
+#endif
 #ifdef SNAPPY_K1R_MSTAMPS
             MSTAMP(m1);
             seg[0] += m1 - m0;
@@ -912,13 +947,13 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     if (lane == 0) {
         uint64_t *st = reinterpret_cast<uint64_t *>(tokens + (uint64_t)gridDim.x * tok_cap) + 4 * (uint64_t)u;
         st[0] = clock64() - t_loop;
-#if defined(SNAPPY_K1R_STAMPS) || defined(SNAPPY_K1R_MSTAMPS)
+#if defined(SNAPPY_K1R_STAMPS) || defined(SNAPPY_K1R_MSTAMPS) || defined(SNAPPY_K1R_FSTAMPS)
         t_match = seg[0] | (seg[1] << 16 << 16);
         st[3] = seg[2] | (seg[3] << 32);
         st[2] = seg[4];
 #endif
         st[1] = t_match;
-#if !defined(SNAPPY_K1R_STAMPS) && !defined(SNAPPY_K1R_MSTAMPS)
+#if !defined(SNAPPY_K1R_STAMPS) && !defined(SNAPPY_K1R_MSTAMPS) && !defined(SNAPPY_K1R_FSTAMPS)
         st[2] = n_probe | ((uint64_t)n_round << 32);
         st[3] = n_match;
 #endif

@@ -94,6 +94,10 @@ _SIGS = {
                                               _c.POINTER(_c.c_size_t)]),
     # FILE* in, header value, FILE* out, bytes read (C stdio streams; used by the C host layer)
     "snappy_amd_host_compress_file": (_c.c_int, [_c.c_void_p, _c.c_uint64, _c.c_void_p, _c.POINTER(_c.c_uint64)]),
+    # reference Buffer cursor helpers (Buffer* is a struct of two pointers and a u32)
+    "init_Buffer": (None, [_c.c_void_p, _c.c_uint]),
+    "move_current": (None, [_c.c_void_p, _c.c_uint]),
+    "reset": (None, [_c.c_void_p]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -85,3 +85,22 @@ def test_reference_cli_links_against_library(tmp_path):
                         f"{src}/result.c", "-L", os.path.dirname(snappy_amd.LIB_PATH), "-lsnappy_amd"],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_buffer_cursor_helpers():
+    # src/buffer_compression.c:10-34 semantics, host-only (no GPU call)
+    import ctypes
+
+    class Buffer(ctypes.Structure):
+        _fields_ = [("current", ctypes.c_void_p), ("beginning", ctypes.c_void_p), ("bytes_left", ctypes.c_uint)]
+
+    lib = snappy_amd.lib()
+    b = Buffer()
+    lib.init_Buffer(ctypes.byref(b), 100)
+    assert b.current == b.beginning and b.current and b.bytes_left == 100
+    assert ctypes.string_at(b.beginning, 100) == bytes(100)  # calloc'd
+    lib.move_current(ctypes.byref(b), 30)
+    assert b.current - b.beginning == 30 and b.bytes_left == 70
+    lib.reset(ctypes.byref(b))
+    assert b.current == b.beginning and b.bytes_left == 70  # reset leaves bytes_left alone
+    ctypes.CDLL(None).free(ctypes.c_void_p(b.beginning))

@@ -43,7 +43,12 @@ WORKLOADS = {
                 "1 GiB/GPU synthetic text as one snappy_compress() stream of 65,536-byte blocks"),
     "random": ("R", 1, snappy_amd.SINGLE, 65536, "1 GiB/GPU random bytes (all-literal), one stream"),
     "repeat": ("P", 2, snappy_amd.SINGLE, 65536, "1 GiB/GPU 64-byte-period repeat (all-copy), one stream"),
+    # BASELINE configs[4]: decode only, a ~10 GB pre-compressed stream (compressed once, untimed)
+    "decode10g": ("T", 1234, snappy_amd.SINGLE, 65536,
+                  "decode-only: 1 GiB/GPU of text pre-compressed (untimed) into one stream of 65,536-byte blocks"),
 }
+DECODE_ONLY = {"decode10g"}
+DECODE10G_BYTES = (18_500_000_000 // 65536) * 65536  # ratio ~1.85 -> ~10 GB of compressed stream
 
 
 def parse():
@@ -56,6 +61,7 @@ def parse():
     ap.add_argument("--assemble", action="store_true", help="also time the RCCL all-gather of shards")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-e2e", action="store_true", help="skip the PCIe-inclusive host API sample")
+    ap.add_argument("--keep-size", action="store_true", help="decode10g: use --bytes-per-gpu as given")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL, the real path) or gloo (CPU collectives; rehearsal with ranks sharing a GPU)")
     ap.add_argument("--cpu-sample-bytes", type=int, default=1 << 30)
@@ -64,7 +70,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(kind: str, seed: int, chunk: int, layout: int, sample: int) -> dict:
+def cpu_baseline(kind: str, seed: int, chunk: int, layout: int, sample: int, decode_only: bool = False):
     """The oracle (CPU restatement, fixture-verified bit-exact with the
     reference) timed on this host, 1 thread like the reference, wall clock."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -91,7 +97,8 @@ def cpu_baseline(kind: str, seed: int, chunk: int, layout: int, sample: int) -> 
                 break
     except OSError:
         pass
-    base = {"value": round(a.size / (t2 - t0) / 1e6, 2), "unit": "MB/s", "cores": 1, "kind": "port",
+    base = {"value": round(a.size / ((t2 - t1) if decode_only else (t2 - t0)) / 1e6, 2), "unit": "MB/s",
+            "cores": 1, "kind": "port",
             "sample": f"{a.size / 2**20:.0f} MiB of the same workload, compress {a.size / (t1 - t0) / 1e6:.1f} MB/s"
                       f" + decompress {a.size / (t2 - t1) / 1e6:.1f} MB/s, oracle/snappy_oracle.c -O2, 1 thread,"
                       f" {cpu_model}"}
@@ -108,7 +115,8 @@ def cpu_baseline(kind: str, seed: int, chunk: int, layout: int, sample: int) -> 
         back = oracle.decompress_streams(payload, offs, a.size, 65536, threads=threads)
     t2 = time.perf_counter()
     assert np.array_equal(back, a)
-    allc = {"value": round(a.size / (t2 - t0) / 1e6, 2), "unit": "MB/s", "cores": threads, "kind": "port",
+    allc = {"value": round(a.size / ((t2 - t1) if decode_only else (t2 - t0)) / 1e6, 2), "unit": "MB/s",
+            "cores": threads, "kind": "port",
             "compress_MBps": round(a.size / (t1 - t0) / 1e6, 1),
             "decompress_MBps": round(a.size / (t2 - t1) / 1e6, 1)}
     return base, allc
@@ -182,7 +190,10 @@ def main():
     cdev = torch.device("cpu") if gloo else dev  # where collective tensors live
 
     kind, seed, layout, chunk, desc = WORKLOADS[args.workload]
+    decode_only = args.workload in DECODE_ONLY
     n = args.bytes_per_gpu
+    if decode_only and n == 1 << 30 and not args.keep_size:
+        n = DECODE10G_BYTES
     host = np.empty(n, dtype=np.uint8)
     datagen.fill(host, kind, seed, offset=rank * n, threads=16)
     x = torch.from_numpy(host).to(dev)
@@ -208,7 +219,16 @@ def main():
         else:
             dist.all_gather_into_tensor(dst, src)
 
+    pre_clen = None
+    if decode_only:  # the stream exists before the timed region
+        pre_clen = codec.compress_ptr_ex(x.data_ptr(), n, chunk, layout, flags, header_value, out.data_ptr(),
+                                         offs.data_ptr())
+
     def step():
+        if decode_only:
+            codec.decompress_ptr_ex(out.data_ptr(), offs.data_ptr(), n, chunk, layout, flags, header_value,
+                                    back.data_ptr(), check=False)
+            return pre_clen
         clen = codec.compress_ptr_ex(x.data_ptr(), n, chunk, layout, flags, header_value, out.data_ptr(),
                                      offs.data_ptr())
         if world > 1:  # C1: shard sizes -> global stream offsets
@@ -277,6 +297,8 @@ def main():
     if os.environ.get("SNAPPY_AMD_FORCE_LDS_K1"):
         k1_name = "k1_compress_units"
     cands = [(k1m, k1_name, n + comp_bytes), (k4m, "k4_decompress_units", comp_bytes + n)]
+    if decode_only:
+        cands = cands[1:]
     dom_ms, dom_name, dom_bytes = max(cands)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None
@@ -290,14 +312,15 @@ def main():
     if rank == 0:
         cpu = cpu_all = e2e = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu, cpu_all = cpu_baseline(kind, seed, chunk, layout, min(args.cpu_sample_bytes, n))
-        if world == 1 and not args.no_host_e2e:
+            cpu, cpu_all = cpu_baseline(kind, seed, chunk, layout, min(args.cpu_sample_bytes, n), decode_only)
+        if world == 1 and not args.no_host_e2e and not decode_only:
             e2e = host_end_to_end(kind, seed, min(n, 256 << 20))
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": f"{args.workload}: {desc.replace('1 GiB/GPU', f'{n / 2**30:g} GiB/GPU')}; one step = compress + decompress round trip",
+            "config": {"workload": f"{args.workload}: {desc.replace('1 GiB/GPU', f'{n / 2**30:.4g} GiB/GPU')}; one step = "
+                                   + ("one decode of the stream" if decode_only else "compress + decompress round trip"),
                        "bytes_per_gpu": n, "chunk": chunk, "layout": "STREAMS" if layout else "SINGLE",
                        "units_per_gpu": units, "parallelism": f"dp{world} (block shards)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -307,7 +330,7 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
             "ratio": round(total_in / total_comp, 4),
-            "compress_MBps": round(n / ((k1m + k3m) * 1e-3) / 1e6, 1),
+            "compress_MBps": None if decode_only else round(n / ((k1m + k3m) * 1e-3) / 1e6, 1),
             "decompress_MBps": round(n / (k4m * 1e-3) / 1e6, 1),
             # src/result.c:40 defines decompress speed over the compressed bytes
             "decompress_MBps_ref_definition": round(comp_bytes / (k4m * 1e-3) / 1e6, 1),

@@ -1343,25 +1343,15 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
         const uint32_t tag = x0 & 0xFF;
         uint32_t size, olen, info;  // info: copy offset, or literal header length
         const uint32_t t = tag & 3;
-        if (t == 0) {
+        {  // branch-free tag dispatch (src/snappy_decompression.c:290-333)
             const uint32_t m = tag >> 2;
-            const uint32_t k = m >= 60 ? m - 59 : 0;  // extra length bytes
-            const uint32_t v = k == 0 ? m : (k == 4 ? ((x0 >> 8) | (x1 << 24)) : ((x0 >> 8) & ((1u << (8 * k)) - 1)));
-            olen = v + 1;  // may be huge for garbage candidates: clamped by the checks below
-            info = 1 + k;
-            size = info + olen;
-        } else if (t == 1) {
-            olen = ((tag >> 2) & 7) + 4;
-            info = ((tag >> 5) << 8) | ((x0 >> 8) & 0xFF);
-            size = 2;
-        } else if (t == 2) {
-            olen = (tag >> 2) + 1;
-            info = (x0 >> 8) & 0xFFFF;
-            size = 3;
-        } else {
-            olen = (tag >> 2) + 1;
-            info = (x0 >> 8) | (x1 << 24);
-            size = 5;
+            const uint32_t k = m >= 60 ? m - 59 : 0;  // literal: extra length bytes
+            const uint32_t b4 = (x0 >> 8) | (x1 << 24);
+            const uint32_t lv = k == 0 ? m : (k == 4 ? b4 : (x0 >> 8) & ((1u << (8 * (k & 3))) - 1));
+            const uint32_t c1 = ((tag >> 5) << 8) | ((x0 >> 8) & 0xFF);
+            olen = t == 0 ? lv + 1 : (t == 1 ? (m & 7) + 4 : m + 1);  // garbage lengths are clamped below
+            info = t == 0 ? 1 + k : (t == 1 ? c1 : (t == 2 ? (x0 >> 8) & 0xFFFF : b4));
+            size = t == 0 ? 1 + k + lv + 1 : (t == 1 ? 2 : (t == 2 ? 3 : 5));
         }
         K4STAMP(tb);
         // ---- element chain from lane 0 by pointer doubling: J^k(0) for lane k
@@ -1374,15 +1364,16 @@ __global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restr
         const uint32_t J4 = JUMP(J2, J2);
         const uint32_t J8 = JUMP(J4, J4);
         const uint32_t J16 = JUMP(J8, J8);
-        const uint32_t J32 = JUMP(J16, J16);
-        // (bpermute must run with every lane active: select afterwards)
+        // (bpermute must run with every lane active: select afterwards).  An
+        // element is at least 2 bytes, so 64 positions hold at most 32
+        // elements: lanes >= 32 are out of the batch
         uint32_t pos = 0;
         { const uint32_t g = JUMP(J1, pos); pos = (lane & 1) ? g : pos; }
         { const uint32_t g = JUMP(J2, pos); pos = (lane & 2) ? g : pos; }
         { const uint32_t g = JUMP(J4, pos); pos = (lane & 4) ? g : pos; }
         { const uint32_t g = JUMP(J8, pos); pos = (lane & 8) ? g : pos; }
         { const uint32_t g = JUMP(J16, pos); pos = (lane & 16) ? g : pos; }
-        { const uint32_t g = JUMP(J32, pos); pos = (lane & 32) ? g : pos; }
+        pos = lane < 32 ? pos : 64;
 #undef JUMP
         // lane k < E holds element k of the batch (starts are increasing)
         const uint64_t inwin = __ballot(pos < 64);

@@ -1259,7 +1259,7 @@ __device__ uint64_t g_k4_stats[32768 * 8];
 #define K4STAMP(var) do { } while (0)
 #endif
 
-__global__ __launch_bounds__(64) void k4_decompress_units(const uint8_t *__restrict__ comp,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_decompress_units(const uint8_t *__restrict__ comp,
                                                           const uint64_t *__restrict__ offsets, uint64_t n,
                                                           uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
                                                           uint32_t comp_cap, uint32_t ring, uint8_t *__restrict__ out,

@@ -247,3 +247,62 @@ def test_parallel_index_errors_match_serial(codec):
         assert c1 == c2
         if c1 == 0:
             assert n1 == n2 and np.array_equal(o1, o2)
+
+
+def test_decoder_fuzz_corrupted_streams():
+    """Corrupted / truncated / garbage streams through the host decoder (index walk +
+    K4): never a crash or hang; whenever the GPU path accepts a stream its output is the
+    oracle decoder's output for it."""
+    rng = np.random.default_rng(2024)
+    base = [oracle.compress(datagen.make(k, n, s).tobytes())
+            for k, n, s in (("T", 5000, 1), ("T", 200_000, 2), ("R", 70_000, 3), ("P", 150_000, 4))]
+    cases = []
+    for b in base:
+        a = np.frombuffer(b, dtype=np.uint8)
+        for _ in range(25):
+            c = a.copy()
+            k = int(rng.integers(1, 6))
+            pos = rng.integers(min(3, a.size - 1), a.size, k)
+            c[pos] = rng.integers(0, 256, k, dtype=np.uint8)
+            cases.append(c.tobytes())
+        for cut in rng.integers(1, a.size, 10):
+            cases.append(b[:int(cut)])
+    for n in (17, 1000, 70_000):
+        hdr = snappy_amd.varint_encode(n)
+        cases.append(hdr + rng.integers(0, 256, n // 2, dtype=np.uint8).tobytes())
+    accepted = 0
+    for c in cases:
+        try:
+            got = snappy_amd.decompress(c)
+        except snappy_amd.SnappyError:
+            continue
+        accepted += 1
+        assert got == oracle.decompress(c)
+    assert accepted >= 4  # at least the untouched-prefix style cases decode
+
+
+def test_streams_decoder_fuzz_device(codec):
+    """Byte flips in a STREAMS payload (index kept): the block-parallel decoder
+    reports a per-unit error or decodes exactly what the oracle decodes for that unit."""
+    import torch
+    chunk = 32768
+    a = datagen.make("T", 64 * chunk, 77)
+    comp, offs = codec.compress_tensor(to_dev(a), chunk=chunk, layout=snappy_amd.STREAMS)
+    raw = comp.cpu().numpy()
+    o = offs.cpu().numpy().astype(np.int64)
+    rng = np.random.default_rng(99)
+    for trial in range(6):
+        c = raw.copy()
+        pos = rng.integers(0, raw.size, 40)
+        c[pos] ^= rng.integers(1, 256, 40, dtype=np.uint8)
+        d = torch.from_numpy(c).cuda()
+        try:
+            back = codec.decompress_tensor(d, offs, a.size, chunk=chunk, layout=snappy_amd.STREAMS)
+            ok = True
+        except snappy_amd.SnappyError:
+            ok = False
+        if ok:  # every unit decoded: each must equal the oracle's decode of that unit
+            got = back.cpu().numpy()
+            for u in range(64):
+                want = oracle.decompress(c[o[u]:o[u + 1]].tobytes())
+                assert got[u * chunk:(u + 1) * chunk].tobytes() == want

@@ -303,21 +303,24 @@ __global__ __launch_bounds__(64) void k1_compress_units(const uint8_t *__restric
 //    the next VGPR's first dword, so any 2 consecutive dwords sit in one
 //    VGPR (a wave-uniform unaligned BE32 is one s_set_gpr_idx + v_mov +
 //    v_readlanes) and any 64 consecutive dwords span two VGPRs.
-//  * The hash table is u32 in LDS (16 KiB): position (low 16 bits) and a
-//    16-bit tag of the 4 bytes there (high 16 bits).  A probe whose tag
-//    differs is a miss decided without touching the input; equal tags are
-//    verified against the bytes, so the probe/insert sequence of
-//    src/snappy_compression.c:384-403 is reproduced bit for bit.
+//  * The hash table lives in LDS as 4096 u16 positions + 4096 u8 tags of the
+//    4 bytes there (12 KiB).  A probe whose tag differs is a miss decided
+//    without touching the input; equal tags are verified against the bytes,
+//    so the probe/insert sequence of src/snappy_compression.c:384-403 is
+//    reproduced bit for bit.
 //  * Hash and tag of 64 consecutive positions are precomputed lane-parallel
-//    (`hv`, lane l <-> position q0 + l) together with their BE32 (`bv`).
-//  * Each round speculates that the next W probes miss: lane k computes its
-//    probe position in closed form, fetches hash/tag by ds_bpermute and its
-//    table slot by one ds_read; a ballot finds the first tag hit, window
-//    conflict or end.  Earlier lanes are exact misses (inserted in lane
-//    order), the hit is verified against the bytes in registers.
-//  * Output is a token list (pos | len << 16, offset) plus the unit's exact
-//    encoded size; K2 writes the bytes once K3 has placed every unit.
-// VGPR budget <= 168 -> 3 waves per SIMD; LDS 16 KiB -> 10 units per CU.
+//    (`hv`, lane l <-> position q0 + l) together with their BE32 (`bv`), from
+//    a 256-byte dword window (`dv`) refreshed every ~136 bytes.
+//  * Each round speculates that the next W = 4 probes miss: lane k computes
+//    its probe position in closed form (p + k after a match), fetches
+//    hash/tag by ds_bpermute and its table slot by one read; a ballot finds
+//    the first tag hit, window conflict or end.  Earlier lanes are exact
+//    misses (inserted in lane order: the highest lane wins a shared slot),
+//    the hit is verified against the bytes in registers.
+//  * Output is a token list (pos | len << 16, offset); K2s sizes it, K3 places
+//    every unit, K2 writes the bytes.
+// 156 VGPRs -> 3 waves per SIMD; 12 KiB LDS -> 12 units per CU (the VGPR limit).
+// 65,536-byte blocks (k1r_match_units64) continue the layout in 130 AGPRs.
 // ---------------------------------------------------------------------------
 typedef uint32_t v32 __attribute__((ext_vector_type(32)));
 typedef uint32_t v3u __attribute__((ext_vector_type(3)));

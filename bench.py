@@ -122,6 +122,30 @@ def cpu_baseline(kind: str, seed: int, chunk: int, layout: int, sample: int, dec
     return base, allc
 
 
+def cpu_reference(kind: str, seed: int, chunk: int, layout: int, sample: int, decode_only: bool = False):
+    """The compiled reference itself (oracle/_ref/libsnappy_ref.so, built from
+    /root/reference/src by oracle/Makefile; its FILE* API through tmpfiles, as
+    cmd.c drives it), 1 thread, on a sample of the same workload.  None when the
+    library is absent."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the CPU baseline leg only
+
+    if not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libsnappy_ref.so")):
+        return None
+    a = datagen.make(kind, sample, seed)
+    step = chunk if layout == snappy_amd.STREAMS else a.size
+    t0 = time.perf_counter()
+    comp = [oracle.ref_compress(a[i:i + step]) for i in range(0, a.size, step)]
+    t1 = time.perf_counter()
+    back = [oracle.ref_decompress(c, min(step, a.size - i * step)) for i, c in enumerate(comp)]
+    t2 = time.perf_counter()
+    assert b"".join(back) == a.tobytes()
+    return {"value": round(a.size / ((t2 - t1) if decode_only else (t2 - t0)) / 1e6, 2), "unit": "MB/s",
+            "cores": 1, "kind": "reference",
+            "sample": f"{a.size / 2**20:.0f} MiB, compress {a.size / (t1 - t0) / 1e6:.1f} MB/s + decompress "
+                      f"{a.size / (t2 - t1) / 1e6:.1f} MB/s, reference src/*.c -O2 through its FILE* API (tmpfiles)"}
+
+
 def host_end_to_end(kind: str, seed: int, sample: int) -> dict:
     """PCIe-inclusive rate of the drop-in host API (snappy_compress_buffer /
     snappy_decompress_buffer: one SINGLE stream of 64 KiB blocks, pageable
@@ -310,9 +334,10 @@ def main():
         pass
 
     if rank == 0:
-        cpu = cpu_all = e2e = None
+        cpu = cpu_all = cpu_ref = e2e = None
         if world == 1 and not args.no_cpu_baseline:
             cpu, cpu_all = cpu_baseline(kind, seed, chunk, layout, min(args.cpu_sample_bytes, n), decode_only)
+            cpu_ref = cpu_reference(kind, seed, chunk, layout, min(128 << 20, n), decode_only)
         if world == 1 and not args.no_host_e2e and not decode_only:
             e2e = host_end_to_end(kind, seed, min(n, 256 << 20))
         line = {
@@ -329,6 +354,7 @@ def main():
                          "algorithmic_bytes_per_launch": dom_bytes},
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
+            "cpu_reference": cpu_ref,
             "ratio": round(total_in / total_comp, 4),
             "compress_MBps": None if decode_only else round(n / ((k1m + k3m) * 1e-3) / 1e6, 1),
             "decompress_MBps": round(n / (k4m * 1e-3) / 1e6, 1),

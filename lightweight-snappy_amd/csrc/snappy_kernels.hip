@@ -1463,15 +1463,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_de
             const bool ex = lane < nexec;
             const uint32_t kop = e_op | (e_t == 0 ? 0x80000000u : 0u);
             const uint32_t kinfo = e_t == 0 ? e_lsrc : e_info;
+#ifdef SNAPPY_K4_BITMAP
             const uint32_t mlo = lane >= 31 ? 0xFFFFFFFFu : (2u << lane) - 1;
             const uint32_t mhi = lane < 32 ? 0u : (lane == 63 ? 0xFFFFFFFFu : (2u << (lane - 32)) - 1);
+#endif
             for (uint32_t P = op; P < op_end; P += 64) {
                 const uint32_t j = e_op - P;
                 const bool inw = ex && j < 64;
+                const uint32_t cb = (uint32_t)__builtin_popcountll(__ballot(ex && e_op < P));
+#ifdef SNAPPY_K4_BITMAP
                 const uint32_t slo = wave_or(inw && j < 32 ? 1u << (j & 31) : 0u);
                 const uint32_t shi = wave_or(inw && j >= 32 ? 1u << (j & 31) : 0u);
-                const uint32_t cb = (uint32_t)__builtin_popcountll(__ballot(ex && e_op < P));
                 const uint32_t id = cb + __builtin_popcount(slo & mlo) + __builtin_popcount(shi & mhi) - 1;
+#else
+                // scatter (element index + 1) onto the byte lane where it starts:
+                // ds_permute delivers 0 to untargeted lanes and the highest sender
+                // wins a collision, so the element lanes are first reversed around
+                // cb (the pass's elements land on the highest lanes; every other
+                // lane sends 0); an inclusive max-scan then gives each byte's element
+                const uint32_t pk = (j & 63) | (inw ? (lane + 1) << 8 : 0u);
+                const uint32_t rv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((cb + 63 - lane) & 63) << 2), (int)pk);
+                uint32_t mk = (uint32_t)__builtin_amdgcn_ds_permute((int)((rv & 63) << 2), (int)(rv >> 8));
+                mk = __builtin_elementwise_max(mk, dpp0<0x111, 0xF>(mk));
+                mk = __builtin_elementwise_max(mk, dpp0<0x112, 0xF>(mk));
+                mk = __builtin_elementwise_max(mk, dpp0<0x114, 0xF>(mk));
+                mk = __builtin_elementwise_max(mk, dpp0<0x118, 0xF>(mk));
+                mk = __builtin_elementwise_max(mk, dpp0<0x142, 0xA>(mk));
+                mk = __builtin_elementwise_max(mk, dpp0<0x143, 0xC>(mk));
+                const uint32_t id = (mk > cb ? mk : cb) - 1;
+#endif
                 const uint32_t f_op = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((id & 63) << 2), (int)kop);
                 const uint32_t f_in = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((id & 63) << 2), (int)kinfo);
                 const uint32_t o = P + lane;

@@ -1018,6 +1018,19 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
     return x - v;
 }
 
+// exclusive add-scan over lanes 0..31 only (lanes 32..63 undefined), total of lanes 0..31
+__device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v, uint32_t *total)
+{
+    uint32_t x = v;
+    x += dpp0<0x111, 0xF>(x);
+    x += dpp0<0x112, 0xF>(x);
+    x += dpp0<0x114, 0xF>(x);
+    x += dpp0<0x118, 0xF>(x);
+    x += dpp0<0x142, 0xA>(x);
+    *total = (uint32_t)__builtin_amdgcn_readlane((int)x, 31);
+    return x - v;
+}
+
 // wave-wide OR, uniform result
 __device__ __forceinline__ uint32_t wave_or(uint32_t x)
 {
@@ -1338,10 +1351,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_de
         }
         // ---- lane-parallel candidate parse: an element starting at o + lane
         const uint32_t q = o + lane;  // < 320
-        const uint32_t dA = WIN_DW(q >> 2), dB = WIN_DW((q >> 2) + 1);
+        // the 64 dwords from o / 4 once, then each lane's three
+        const uint32_t w64 = WIN_DW((o >> 2) + lane);
+        const uint32_t kq = ((o & 3) + lane) >> 2;
+        const uint32_t dA = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(kq << 2), (int)w64);
+        const uint32_t dB = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((kq + 1) << 2), (int)w64);
+        const uint32_t dC = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((kq + 2) << 2), (int)w64);
         const uint32_t sh = 8 * (q & 3);
         const uint32_t x0 = sh ? (dA >> sh) | (dB << (32 - sh)) : dA;  // tag, t1, t2, t3
-        const uint32_t dC = WIN_DW((q >> 2) + 2);
         const uint32_t x1 = sh ? (dB >> sh) | (dC << (32 - sh)) : dB;  // t4..t7
         const uint32_t tag = x0 & 0xFF;
         uint32_t size, olen, info;  // info: copy offset, or literal header length
@@ -1390,8 +1407,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_de
         // the batch (64-bit safe: garbage past E is zeroed)
         const bool live = lane < E;
         uint32_t tot_in, tot_out;
-        const uint32_t in_off = wave_excl_scan(live ? e_size : 0, lane, &tot_in);
-        const uint32_t out_off = wave_excl_scan(live ? e_len : 0, lane, &tot_out);
+        const uint32_t in_off = wave_excl_scan32(live ? e_size : 0, &tot_in);  // E <= 32
+        const uint32_t out_off = wave_excl_scan32(live ? e_len : 0, &tot_out);
         // validity in stream order: stop at the first element that runs past the
         // unit (truncated / overrun), reaches before the unit start, or past want
         const uint32_t e_ip = ip + in_off, e_op = op + out_off;

@@ -328,7 +328,7 @@ typedef uint32_t v8u __attribute__((ext_vector_type(8)));
 
 constexpr uint32_t kTagMul = 0x9E3779B1u;
 constexpr uint32_t kRegs = 131;     // VGPRs holding a unit (63 dwords each): dwords < 8253 (32 KiB units)
-constexpr uint32_t kRegsBig = 261;  // 65,536-byte units: 131 VGPRs + 130 AGPRs
+constexpr uint32_t kRegsBig = 261;  // 65,536-byte units: 131 VGPRs + 130 AGPRs (+1 spare AGPR)
 
 // Register r (wave-uniform) of the resident unit.  g0..g4 are pinned to
 // v2..v132 by the asm constraints (65,536-byte units continue in a0..a129),
@@ -367,6 +367,13 @@ constexpr uint32_t kRegsBig = 261;  // 65,536-byte units: 131 VGPRs + 130 AGPRs
         _rv;                                                                                        \
     })
 
+// big-endian funnel: the 32 bits starting s bits (0, 8, 16, 24) into hi:lo;
+// v_alignbit + a select, no branch on s
+__device__ __forceinline__ uint32_t funnel_be(uint32_t hi, uint32_t lo, uint32_t s)
+{
+    return s ? __builtin_amdgcn_alignbit(hi, lo, 32 - s) : hi;
+}
+
 // halo layout: dword d -> register d / 63, lane d % 63 (exact for d < 16700)
 #define HALO_R(d) (((d) * 16645u) >> 20)
 
@@ -394,7 +401,7 @@ constexpr uint32_t kRegsBig = 261;  // 65,536-byte units: 131 VGPRs + 130 AGPRs
         const uint32_t _le = _e - 63 * (_R + _re);                                                     \
         const uint32_t _x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)REG_OF(_R));  \
         const uint32_t _x1 = (uint32_t)__builtin_amdgcn_ds_bpermute(                                   \
-            (int)(_le << 2), (int)(_R + 1 < NREG ? REG_OF(_R + 1) : 0));                               \
+            (int)(_le << 2), (int)REG_OF(_R + 1)); /* R + 1 <= NREG: one spare register */            \
         _re == 0 ? _x0 : _x1;                                                                          \
     })
 
@@ -483,14 +490,14 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
         const uint32_t _e = _d0 + (lane & 15);                                                       \
         const uint32_t _re = HALO_R(_e) - _R; /* 0..1 */                                            \
         const uint32_t _le = _e - 63 * (_R + _re);                                                   \
-        const uint32_t _r0 = REG_OF(_R), _r1 = _R + 1 < NREG ? REG_OF(_R + 1) : 0;                  \
+        const uint32_t _r0 = REG_OF(_R), _r1 = REG_OF(_R + 1);                                      \
         const uint32_t _x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)_r0);      \
         const uint32_t _x1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_le + 1) << 2), (int)_r0);\
         const uint32_t _y0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)_r1);      \
         const uint32_t _y1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_le + 1) << 2), (int)_r1);\
         const uint32_t _hi = _re ? _y0 : _x0, _lo = _re ? _y1 : _x1;                                 \
         const uint32_t _s = 8 * (_q & 3);                                                            \
-        _s ? (_hi << _s) | (_lo >> (32 - _s)) : _hi;                                                 \
+        funnel_be(_hi, _lo, _s);                                                                     \
     })
 
 #ifndef SNAPPY_K1R_WINDOW
@@ -522,6 +529,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 {
     constexpr int W = SNAPPY_K1R_WINDOW;
     constexpr uint32_t NREG = BIG ? kRegsBig : kRegs;
+    (void)NREG;
     (void)hdr_mode;
     (void)header_value;
 #ifndef SNAPPY_K1R_TABLE16
@@ -706,6 +714,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         K1R_AW(127);
         K1R_AW(128);
         K1R_AW(129);
+        K1R_AW(130);  // spare (zeros): gathers may name register R + 1 = 261 without a bounds test
 #undef K1R_AW
     }
 
@@ -740,7 +749,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         const uint32_t _a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_k << 2), (int)dv);       \
         const uint32_t _b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_k + 1) << 2), (int)dv); \
         const uint32_t _s = 8 * ((q0 + lane) & 3);                                                 \
-        bv = _s ? (_a << _s) | (_b >> (32 - _s)) : _a;                                             \
+        bv = funnel_be(_a, _b, _s);                                                                \
         hv = ((bv * kMul) >> shift) | (TAG_OF(bv) << 16);                                          \
     } while (0)
 
@@ -752,7 +761,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         const uint32_t _pa = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_kp << 2), (int)dv);     \
         const uint32_t _pb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_kp + 1) << 2), (int)dv); \
         const uint32_t _ps = 8 * (_pp & 3);                                                        \
-        _ps ? (_pa << _ps) | (_pb >> (32 - _ps)) : _pa;                                            \
+        funnel_be(_pa, _pb, _ps);                                                                  \
     })
 
 #ifdef SNAPPY_K1R_STATS
@@ -843,7 +852,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             const uint32_t _e = _d0 + (lane & 15);
             const uint32_t _re = HALO_R(_e) - _R;
             const uint32_t _le = _e - 63 * (_R + _re);
-            const uint32_t _r0 = REG_OF(_R), _r1 = _R + 1 < NREG ? REG_OF(_R + 1) : 0;
+            const uint32_t _r0 = REG_OF(_R), _r1 = REG_OF(_R + 1);
             asm volatile("" ::"v"(_r0), "v"(_r1));
             MSTAMP(fb);
             const uint32_t pvv = PV_LANES16(pf);
@@ -855,7 +864,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             MSTAMP(fc);
             const uint32_t _hi = _re ? _y0 : _x0, _lo = _re ? _y1 : _x1;
             const uint32_t _s = 8 * (_q & 3);
-            const uint32_t cv = _s ? (_hi << _s) | (_lo >> (32 - _s)) : _hi;
+            const uint32_t cv = funnel_be(_hi, _lo, _s);
             const uint32_t y = (pvv ^ cv) & (uint32_t)(((int32_t)(lane - 16)) >> 31);
             const uint64_t bad = __ballot(y != 0);
             asm volatile("" ::"s"(bad));
@@ -886,8 +895,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute(nx, (int)a0);
                     const uint32_t b1 = (uint32_t)__builtin_amdgcn_ds_bpermute(nx, (int)b0);
                     const uint32_t sa = 8 * (qa & 3), sb = 8 * (qb & 3);
-                    const uint32_t va = sa ? (a0 << sa) | (a1 >> (32 - sa)) : a0;
-                    const uint32_t vb = sb ? (b0 << sb) | (b1 >> (32 - sb)) : b0;
+                    const uint32_t va = funnel_be(a0, a1, sa);
+                    const uint32_t vb = funnel_be(b0, b1, sb);
                     const uint32_t yy = lane < 63 ? (va ^ vb) : 0;  // lane 63 lacks its successor
                     const uint64_t bb = __ballot(yy != 0);
                     if (bb) {

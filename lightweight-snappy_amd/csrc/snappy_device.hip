@@ -206,8 +206,11 @@ static int compress_impl(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t
         const uint32_t hm = hdr_mode_of(layout, flags);
         if (c->timing) (void)hipEventRecord(c->ev[0], c->stream);
         // units <= 32 KiB: unit in VGPRs (3 waves/SIMD); 64 KiB blocks: VGPRs + AGPRs (1 wave/SIMD)
+        // SNAPPY_K1R_DYNLDS=<bytes>: occupancy experiments (extra dynamic LDS per unit)
+        const char *dyn = getenv("SNAPPY_K1R_DYNLDS");
+        const uint32_t dyn_lds = dyn ? (uint32_t)atoi(dyn) : 0;
         if (unit <= SNAPPY_K1R_MAX_UNIT)
-            hipLaunchKernelGGL(k1r_match_units, dim3((uint32_t)units), dim3(64), 0, c->stream,
+            hipLaunchKernelGGL(k1r_match_units, dim3((uint32_t)units), dim3(64), dyn_lds, c->stream,
                                static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens,
                                tok_cap, c->ntok, c->sizes);
         else

@@ -480,6 +480,25 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
     return c;
 }
 
+// DPP wave_shr:1: lane l <- lane l - 1 across the whole wave (lane 0 <- 0)
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);
+}
+
+// bit d (1 <= d <= D) set iff lane l - d carries the same x as lane l (x != 0)
+template <uint32_t D>
+__device__ __forceinline__ uint32_t same_x_bits(uint32_t x)
+{
+    uint32_t xs = x, bits = 0;
+#pragma unroll
+    for (uint32_t d = 1; d <= D; d++) {
+        xs = wave_shr1(xs);
+        bits |= (xs == x) ? (1u << d) : 0u;
+    }
+    return bits;
+}
+
 // per-lane BE32 at q + 4*lane for lanes 0..15 (q uniform): 17 dwords span
 // at most VGPRs R, R+1 of the halo layout
 #define BE32_LANES16(qq)                                                                             \
@@ -500,6 +519,15 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
         funnel_be(_hi, _lo, _s);                                                                     \
     })
 
+#ifndef SNAPPY_K1R_DMAX
+#define SNAPPY_K1R_DMAX 16  // lane-space rounds: same-hash distances resolved per window
+#endif
+#ifndef SNAPPY_K1R_LSMIN
+#define SNAPPY_K1R_LSMIN 4  // lane-space rounds while at least this many step-1 probes remain
+#endif
+#ifndef SNAPPY_K1R_RMIN
+#define SNAPPY_K1R_RMIN 8  // refresh the window when fewer probe lanes remain
+#endif
 #ifndef SNAPPY_K1R_WINDOW
 #define SNAPPY_K1R_WINDOW 4  // 2.6 probes per round on text: 4 speculative lanes suffice
 #endif
@@ -773,10 +801,134 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     uint64_t seg[6] = {0, 0, 0, 0, 0, 0};
     uint64_t s0, s1, s2, s3, s4, s5;
 #endif
+    // ---- lane-space rounds (step-1 probes, the text regime): lane l of the
+    // position window IS probe position q0 + l, so a round needs no gather of
+    // hashes.  Lane l's candidate is the table entry (read after the previous
+    // round's inserts) unless a lane in [lane0 - 1, l) has the same hash: the
+    // misses of this round insert exactly those positions (p - 1, p, ...), so
+    // the nearest such lane is then the candidate.  Same-hash distances up to
+    // DMAX are found once per window (DPP wave_shr chain), so a round can
+    // speculate DMAX probes with no conflict stops.
+    constexpr uint32_t DMAX = SNAPPY_K1R_DMAX;
+    uint32_t pd = 0, pdc = 0, pdt = 0, ent = 0, lmax = 0;
+    bool lsw = false;  // pd/pdc/pdt/ent describe the current window
+#define WINDOW_LS(qq)                                                                              \
+    do {                                                                                           \
+        WINDOW_AT(qq);                                                                             \
+        const uint32_t _bits = same_x_bits<DMAX>((hv & 0xFFFF) + 1);                               \
+        pd = _bits ? (uint32_t)__builtin_ctz(_bits) : 0xFFFFFFFFu;                                 \
+        pdc = q0 + lane - pd;                                                                      \
+        const uint32_t _hp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - pd) & 63) << 2), (int)hv); \
+        pdt = _hp == hv ? 1u : 0u;                                                                 \
+        /* probe lanes keep the verification's dwords inside dv: pf / 4 <= d0 + 47 */             \
+        lmax = 4 * d0 + 191 - q0;                                                                  \
+        lmax = lmax < 62 ? lmax : 62;                                                              \
+        ent = TBL_READ(hv & 0xFFFF);                                                               \
+        lsw = true;                                                                                \
+    } while (0)
+
+    // find_copy_length :61-72 after found_match :259-265: common prefix of the
+    // bytes at pf and cand (lanes 0..15 compare 64 bytes, then 252 per pass)
+    auto match_len = [&](uint32_t pf, uint32_t cand) -> uint32_t {
+        const uint32_t y = (PV_LANES16(pf) ^ BE32_LANES16(cand)) & (uint32_t)(((int32_t)(lane - 16)) >> 31);
+        const uint64_t bad = __ballot(y != 0);
+        uint32_t len;
+        if (bad) {
+            const uint32_t m = (uint32_t)__builtin_ctzll(bad);
+            len = 4 * m + ((uint32_t)__builtin_clz(__builtin_amdgcn_readlane(y, m)) >> 3);
+        } else {
+            len = 64;
+            for (;;) {
+                if (pf + len >= L) break;
+                const uint32_t qa = pf + len, qb = cand + len;
+                const uint32_t a0 = DW_LANES(qa >> 2), b0 = DW_LANES(qb >> 2);
+                const int nx = (int)(((lane + 1) & 63) << 2);
+                const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute(nx, (int)a0);
+                const uint32_t b1 = (uint32_t)__builtin_amdgcn_ds_bpermute(nx, (int)b0);
+                const uint32_t va = funnel_be(a0, a1, 8 * (qa & 3));
+                const uint32_t vb = funnel_be(b0, b1, 8 * (qb & 3));
+                const uint32_t yy = lane < 63 ? (va ^ vb) : 0;
+                const uint64_t bb = __ballot(yy != 0);
+                if (bb) {
+                    const uint32_t m = (uint32_t)__builtin_ctzll(bb);
+                    len += 4 * m + ((uint32_t)__builtin_clz(__builtin_amdgcn_readlane(yy, m)) >> 3);
+                    break;
+                }
+                len += 252;
+            }
+        }
+        return len;
+    };
+
     uint32_t p = 1, skip = 33;
     while (!(L - p < (skip >> 5) + 15)) {  // is_block_end :229-232
 #ifdef SNAPPY_K1R_STATS
         n_round++;
+#endif
+#ifndef SNAPPY_K1R_LEGACY
+        if (skip <= 64 - SNAPPY_K1R_LSMIN) {
+            uint32_t lane0 = p - q0;
+            if (!lsw || p - 1 < q0 || lane0 + SNAPPY_K1R_RMIN > lmax) {
+                WINDOW_LS(p - 1);
+                lane0 = 1;
+            }
+            // last speculative offset k: step 1 ((skip + k - 1) >> 5 == 1 before it),
+            // predecessors within DMAX, inside the window, not past is_block_end
+            uint32_t kmax = 64 - skip;
+            kmax = kmax < DMAX - 1 ? kmax : DMAX - 1;
+            kmax = kmax < lmax - lane0 ? kmax : lmax - lane0;
+            kmax = kmax < L - p - 16 ? kmax : L - p - 16;
+            if (skip + kmax == 64 && L - p - kmax < 17) kmax--;
+            const uint32_t k = lane - lane0;
+            // lane0's own lookup precedes every insert of the round
+            const bool inr = pd <= k + 1 && k != 0;
+            const uint32_t cand = inr ? pdc : (ent & 0xFFFF);
+            const bool hit = inr ? (pdt != 0) : (((ent ^ hv) >> 16) == 0);
+            const uint64_t hm = __ballot(k <= kmax && hit);
+            uint32_t lo = lane0 - 1, hi, np;
+            if (hm) {
+                const uint32_t f = (uint32_t)__builtin_ctzll(hm);
+                const uint32_t pf = q0 + f;
+                const uint32_t c = __builtin_amdgcn_readlane(cand, f);
+                uint32_t len = match_len(pf, c);
+                hi = f;
+#ifdef SNAPPY_K1R_STATS
+                n_probe += f - lane0 + 1;
+#endif
+                if (len >= 4) {  // emit_copy :323-329 (the table insert of pf is lane f's)
+                    if (len > L - pf) len = L - pf;
+#ifdef SNAPPY_K1R_STATS
+                    n_match++;
+#endif
+                    tka = (uint32_t)amdgcn_writelane((int)(pf | (len << 16)), (int)(nt & 63), (int)tka);
+                    tkb = (uint32_t)amdgcn_writelane((int)(pf - c), (int)(nt & 63), (int)tkb);
+                    nt++;
+                    if ((nt & 63) == 0) tok[nt - 64 + lane] = make_uint2(tka, tkb);
+                    if (f == lane0) lo = lane0;  // a first-probe match inserts no p - 1
+                    np = pf + len;
+                    skip = 32;
+                } else {  // tag collision: a miss (append_literal :283-287 steps by skip >> 5)
+                    np = pf + ((skip + f - lane0) >> 5);
+                    skip += f - lane0 + 1;
+                }
+            } else {
+                const uint32_t f = lane0 + kmax + 1;
+                hi = f - 1;
+                np = q0 + f - 1 + ((skip + kmax) >> 5);  // the last probe steps by 2 at skip 64
+                skip += kmax + 1;
+#ifdef SNAPPY_K1R_STATS
+                n_probe += kmax + 1;
+#endif
+            }
+            // update_hash_table :303-307 for the misses (p_k - 1 and p_k) and the
+            // match's own slot: every position of [lo, hi] once, the highest lane
+            // (latest position) winning a shared slot
+            if (lane - lo <= hi - lo) TBL_WRITE(hv & 0xFFFF, (q0 + lane) | (hv & 0xFFFF0000u));
+            ent = TBL_READ(hv & 0xFFFF);
+            p = np;
+            continue;
+        }
+        lsw = false;
 #endif
         STAMP(s0);
         if (p - 1 < q0 || p + 12 > q0 + 64) WINDOW_AT(p - 1);
@@ -948,6 +1100,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         SEG(4, s4, s5);
     }
 #undef WINDOW_AT
+#undef WINDOW_LS
 #undef PV_LANES16
 #undef TAG_OF
 #undef TBL_READ

@@ -295,43 +295,47 @@ __global__ __launch_bounds__(64) void k1_compress_units(const uint8_t *__restric
 }
 
 // ---------------------------------------------------------------------------
-// K1r: register-resident match finder for units <= 32 KiB (the STREAMS
-// layout of BASELINE.json configs[1]).
+// K1r: register-resident match finder (one wave per unit).
 //
-//  * The unit lives in 131 VGPRs of its wave (v2..v132), "halo" layout:
-//    VGPR r, lane l < 63 holds big-endian dword 63 r + l and lane 63 repeats
-//    the next VGPR's first dword, so any 2 consecutive dwords sit in one
-//    VGPR (a wave-uniform unaligned BE32 is one s_set_gpr_idx + v_mov +
-//    v_readlanes) and any 64 consecutive dwords span two VGPRs.
+//  * The unit lives in VGPRs: register r, lane l holds big-endian dword
+//    64 r + l (128 VGPRs v2..v129 for 32 KiB; 65,536-byte blocks continue in
+//    AGPRs a0..a127 + zero spare a128).  A wave-uniform
+//    register index goes through s_set_gpr_idx_on.  Any 64 consecutive dwords
+//    d..d+63 sit in registers R = d / 64 and R + 1: merged by one lane select
+//    they are a rotation of the wanted lanes, undone by one ds_bpermute.
 //  * The hash table lives in LDS as 4096 u16 positions + 4096 u8 tags of the
 //    4 bytes there (12 KiB).  A probe whose tag differs is a miss decided
 //    without touching the input; equal tags are verified against the bytes,
 //    so the probe/insert sequence of src/snappy_compression.c:384-403 is
 //    reproduced bit for bit.
-//  * Hash and tag of 64 consecutive positions are precomputed lane-parallel
-//    (`hv`, lane l <-> position q0 + l) together with their BE32 (`bv`), from
-//    a 256-byte dword window (`dv`) refreshed every ~136 bytes.
-//  * Each round speculates that the next W = 4 probes miss: lane k computes
-//    its probe position in closed form (p + k after a match), fetches
-//    hash/tag by ds_bpermute and its table slot by one read; a ballot finds
-//    the first tag hit, window conflict or end.  Earlier lanes are exact
-//    misses (inserted in lane order: the highest lane wins a shared slot),
-//    the hit is verified against the bytes in registers.
+//  * Position window: lane l <-> position q0 + l holds the BE32 there (`bv`),
+//    its hash and tag (`hv`), the nearest earlier window lane with the same
+//    hash (DPP wave_shr chain, up to DMAX back) and the table entry of its
+//    slot (`ent`, re-read after every round's inserts).
+//  * Lane-space rounds (step-1 probes, i.e. skip < 64: the text regime): the
+//    probes p, p + 1, ... ARE window lanes p - q0, ...  Lane l's candidate is
+//    its table entry unless a lane in [p - 1 - q0, l) has the same hash (the
+//    round's misses insert exactly those positions): then that lane.  One
+//    ballot finds the first probable hit; the lanes before it are exact
+//    misses, inserted by one lane-ordered write (the highest lane wins a
+//    shared slot, which is the serial order); the hit is verified and its
+//    length found by 16 lanes comparing 64 bytes per step.
+//  * Larger steps (skip >= 61, incompressible data) use W = 4 speculative
+//    probes at their closed-form positions with explicit conflict stops.
 //  * Output is a token list (pos | len << 16, offset); K2s sizes it, K3 places
 //    every unit, K2 writes the bytes.
-// 156 VGPRs -> 3 waves per SIMD; 12 KiB LDS -> 12 units per CU (the VGPR limit).
-// 65,536-byte blocks (k1r_match_units64) continue the layout in 130 AGPRs.
+// 12 KiB LDS and <= 168 VGPRs -> 12 units per CU (3 waves per SIMD);
+// 65,536-byte blocks (k1r_match_units64): 1 wave per SIMD.
 // ---------------------------------------------------------------------------
 typedef uint32_t v32 __attribute__((ext_vector_type(32)));
-typedef uint32_t v3u __attribute__((ext_vector_type(3)));
-typedef uint32_t v8u __attribute__((ext_vector_type(8)));
+typedef uint32_t __attribute__((aligned(1))) u32u;
+typedef uint16_t __attribute__((aligned(1))) u16u;
 
 constexpr uint32_t kTagMul = 0x9E3779B1u;
-constexpr uint32_t kRegs = 131;     // VGPRs holding a unit (63 dwords each): dwords < 8253 (32 KiB units)
-constexpr uint32_t kRegsBig = 261;  // 65,536-byte units: 131 VGPRs + 130 AGPRs (+1 spare AGPR)
+constexpr uint32_t kRegs = 128;  // VGPRs holding a 32 KiB unit (64 dwords each), + 1 zero spare
 
-// Register r (wave-uniform) of the resident unit.  g0..g4 are pinned to
-// v2..v132 by the asm constraints (65,536-byte units continue in a0..a129),
+// Register r (wave-uniform) of the resident unit.  g0..g3 are pinned to
+// v2..v129 by the asm constraints (65,536-byte units continue in a0..a128),
 // so the relative move (s_set_gpr_idx_on, SRC0) is exact whatever else the
 // allocator does; AGPRs are read with v_accvgpr_read.
 #define REG_OF_V(r)                                                                                 \
@@ -340,10 +344,10 @@ constexpr uint32_t kRegsBig = 261;  // 65,536-byte units: 131 VGPRs + 130 AGPRs 
         asm volatile("s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\tv_mov_b32 %0, v2\n\ts_set_gpr_idx_off"      \
                      : "=&v"(_v)                                                                    \
                      : "s"((uint32_t)(r)), "{v[2:33]}"(g0), "{v[34:65]}"(g1), "{v[66:97]}"(g2),          \
-                       "{v[98:129]}"(g3), "{v[130:132]}"(g4));                                      \
+                       "{v[98:129]}"(g3));                                                          \
         _v;                                                                                         \
     })
-// AGPRs a0..a129 are written once by the prologue's v_accvgpr_write asm
+// AGPRs a0..a128 are written once by the prologue's v_accvgpr_write asm
 // (with the registers as clobbers, so the kernel allocates them) and are
 // otherwise invisible to the compiler, which never needs AGPRs here
 #define REG_OF_A(r)                                                                                 \
@@ -367,43 +371,51 @@ constexpr uint32_t kRegsBig = 261;  // 65,536-byte units: 131 VGPRs + 130 AGPRs 
         _rv;                                                                                        \
     })
 
-// big-endian funnel: the 32 bits starting s bits (0, 8, 16, 24) into hi:lo;
-// v_alignbit + a select, no branch on s
-__device__ __forceinline__ uint32_t funnel_be(uint32_t hi, uint32_t lo, uint32_t s)
+// lane i <- big-endian dword d + i of the unit (d wave-uniform): registers
+// R = d / 64 and R + 1 merged at lane d % 64 hold the 64 dwords rotated by
+// d % 64; one ds_bpermute puts them in order
+#define DW_LANES(dd)                                                                                 \
+    ({                                                                                               \
+        const uint32_t _d = (dd);                                                                    \
+        const uint32_t _R = _d >> 6, _l0 = _d & 63;                                                  \
+        /* R + 1 = 128 (v130, 32 KiB units) holds no unit data: those lanes lie past the */          \
+        /* unit end, where every caller ignores them (past-L compares are clamped) */              \
+        const uint32_t _r0 = REG_OF(_R), _r1 = REG_OF(_R + 1);                                       \
+        const uint32_t _m = lane >= _l0 ? _r0 : _r1;                                                 \
+        (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((_l0 + lane) & 63) << 2), (int)_m);            \
+    })
+
+// DPP across the whole wave: wave_shl:1 (lane l <- l + 1) and wave_shr:1
+// (lane l <- l - 1); lanes with no source get 0
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t v)
 {
-    return s ? __builtin_amdgcn_alignbit(hi, lo, 32 - s) : hi;
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);
 }
 
-// halo layout: dword d -> register d / 63, lane d % 63 (exact for d < 16700)
-#define HALO_R(d) (((d) * 16645u) >> 20)
+// big-endian funnel by bytes: the 32 bits starting k bytes (0..3) into the
+// 64-bit big-endian hi:lo, one v_perm_b32 (selector bytes 4-k..7-k)
+__device__ __forceinline__ uint32_t perm_sel(uint32_t k) { return 0x07060504u - k * 0x01010101u; }
+__device__ __forceinline__ uint32_t funnel_bytes(uint32_t hi, uint32_t lo, uint32_t sel)
+{
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
 
-// BE32 load at byte q (src/snappy_compression.c:239-241), q wave-uniform
-#define BE32_REG(qq)                                                        \
-    ({                                                                      \
-        const uint32_t _q = (qq);                                           \
-        const uint32_t _d = _q >> 2;                                        \
-        const uint32_t _r = HALO_R(_d);                                     \
-        const uint32_t _l = _d - 63 * _r;                                   \
-        const uint32_t _v = REG_OF(_r);                                     \
-        const uint32_t _hi = __builtin_amdgcn_readlane(_v, _l);             \
-        const uint32_t _lo = __builtin_amdgcn_readlane(_v, _l + 1);         \
-        (uint32_t)(((((uint64_t)_hi) << 32 | _lo) << (8 * (_q & 3))) >> 32); \
-    })
-
-// per-lane dword e = d0 + lane (d0 uniform): the 64 dwords span VGPRs R, R+1
-// of the halo layout
-#define DW_LANES(dd0)                                                                                  \
-    ({                                                                                                 \
-        const uint32_t _d0 = (dd0);                                                                    \
-        const uint32_t _R = HALO_R(_d0);                                                               \
-        const uint32_t _e = _d0 + lane;                                                                \
-        const uint32_t _re = HALO_R(_e) - _R; /* 0..1 */                                              \
-        const uint32_t _le = _e - 63 * (_R + _re);                                                     \
-        const uint32_t _x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)REG_OF(_R));  \
-        const uint32_t _x1 = (uint32_t)__builtin_amdgcn_ds_bpermute(                                   \
-            (int)(_le << 2), (int)REG_OF(_R + 1)); /* R + 1 <= NREG: one spare register */            \
-        _re == 0 ? _x0 : _x1;                                                                          \
-    })
+// bit d (1 <= d <= D) set iff lane l - d carries the same x as lane l (x != 0)
+template <uint32_t D>
+__device__ __forceinline__ uint32_t same_x_bits(uint32_t x)
+{
+    uint32_t xs = x, bits = 0;
+#pragma unroll
+    for (uint32_t d = 1; d <= D; d++) {
+        xs = wave_shr1(xs);
+        bits |= (xs == x) ? (1u << d) : 0u;
+    }
+    return bits;
+}
 
 __device__ __forceinline__ uint32_t varint_len(uint64_t v)
 {
@@ -428,16 +440,12 @@ __device__ __forceinline__ uint32_t copy_bytes(uint32_t len, uint32_t off)
     return 3 * (n64 + has60) + ((last < 12 && off < 2048) ? 2 : 3);
 }
 
-// Window conflicts under the tagged table with lane-ordered inserts (the
-// highest lane of one ds_write wins a shared slot, which is the serial
-// order): lane k must not read a slot an earlier lane writes (h_k in
-// {h_j, a_j}), nor have its a-insert overwritten by an earlier lane's
-// h-insert of another position (a_k == h_j, p_j != p_k - 1).
-// Everything stays in VALU integer ops (a bool in a lane mask would bounce
-// through SGPRs on every compare): eqm(x) = all-ones iff x == 0, for x < 2^31.
-// Lanes with no source lane see 0 (bound_ctrl), which can only add false
-// conflicts; lane 0 is never flagged (the caller masks it), so every round
-// makes progress.
+// Conflicts of the W-probe rounds (large steps): lane k must not read a slot
+// an earlier lane writes (h_k in {h_j, a_j}), nor have its a-insert
+// overwritten by an earlier lane's h-insert of another position (a_k == h_j,
+// p_j != p_k - 1).  eqm(x) = all-ones iff x == 0, for x < 2^31.  Lanes with no
+// source lane see 0 (bound_ctrl), which can only add false conflicts; lane 0
+// is never flagged (the caller masks it), so every round makes progress.
 __device__ __forceinline__ uint32_t eqm(uint32_t x) { return (uint32_t)((int32_t)(x - 1) >> 31); }
 
 template <int N>
@@ -457,67 +465,13 @@ __device__ __forceinline__ uint32_t tconf_step(uint32_t h, uint32_t a, uint32_t 
 template <int W>
 __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdup)
 {
+    static_assert(W >= 1 && W <= 4, "W-probe rounds speculate at most 4 probes");
     uint32_t c = 0;
     if constexpr (W > 1) c |= tconf_step<1>(h, a, notdup);
     if constexpr (W > 2) c |= tconf_step<2>(h, a, notdup);
     if constexpr (W > 3) c |= tconf_step<3>(h, a, notdup);
-    if constexpr (W > 4) {
-        c |= tconf_step<4>(h, a, notdup);
-        c |= tconf_step<5>(h, a, notdup);
-        c |= tconf_step<6>(h, a, notdup);
-        c |= tconf_step<7>(h, a, notdup);
-    }
-    if constexpr (W > 8) {
-        c |= tconf_step<8>(h, a, notdup);
-        c |= tconf_step<9>(h, a, notdup);
-        c |= tconf_step<10>(h, a, notdup);
-        c |= tconf_step<11>(h, a, notdup);
-        c |= tconf_step<12>(h, a, notdup);
-        c |= tconf_step<13>(h, a, notdup);
-        c |= tconf_step<14>(h, a, notdup);
-        c |= tconf_step<15>(h, a, notdup);
-    }
     return c;
 }
-
-// DPP wave_shr:1: lane l <- lane l - 1 across the whole wave (lane 0 <- 0)
-__device__ __forceinline__ uint32_t wave_shr1(uint32_t v)
-{
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);
-}
-
-// bit d (1 <= d <= D) set iff lane l - d carries the same x as lane l (x != 0)
-template <uint32_t D>
-__device__ __forceinline__ uint32_t same_x_bits(uint32_t x)
-{
-    uint32_t xs = x, bits = 0;
-#pragma unroll
-    for (uint32_t d = 1; d <= D; d++) {
-        xs = wave_shr1(xs);
-        bits |= (xs == x) ? (1u << d) : 0u;
-    }
-    return bits;
-}
-
-// per-lane BE32 at q + 4*lane for lanes 0..15 (q uniform): 17 dwords span
-// at most VGPRs R, R+1 of the halo layout
-#define BE32_LANES16(qq)                                                                             \
-    ({                                                                                               \
-        const uint32_t _q = (qq);                                                                    \
-        const uint32_t _d0 = _q >> 2;                                                                \
-        const uint32_t _R = HALO_R(_d0);                                                             \
-        const uint32_t _e = _d0 + (lane & 15);                                                       \
-        const uint32_t _re = HALO_R(_e) - _R; /* 0..1 */                                            \
-        const uint32_t _le = _e - 63 * (_R + _re);                                                   \
-        const uint32_t _r0 = REG_OF(_R), _r1 = REG_OF(_R + 1);                                      \
-        const uint32_t _x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)_r0);      \
-        const uint32_t _x1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_le + 1) << 2), (int)_r0);\
-        const uint32_t _y0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)_r1);      \
-        const uint32_t _y1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_le + 1) << 2), (int)_r1);\
-        const uint32_t _hi = _re ? _y0 : _x0, _lo = _re ? _y1 : _x1;                                 \
-        const uint32_t _s = 8 * (_q & 3);                                                            \
-        funnel_be(_hi, _lo, _s);                                                                     \
-    })
 
 #ifndef SNAPPY_K1R_DMAX
 #define SNAPPY_K1R_DMAX 16  // lane-space rounds: same-hash distances resolved per window
@@ -529,52 +483,50 @@ __device__ __forceinline__ uint32_t same_x_bits(uint32_t x)
 #define SNAPPY_K1R_RMIN 8  // refresh the window when fewer probe lanes remain
 #endif
 #ifndef SNAPPY_K1R_WINDOW
-#define SNAPPY_K1R_WINDOW 4  // 2.6 probes per round on text: 4 speculative lanes suffice
+#define SNAPPY_K1R_WINDOW 4  // W-probe rounds
 #endif
 
-#if defined(SNAPPY_K1R_STAMPS) || defined(SNAPPY_K1R_MSTAMPS) || defined(SNAPPY_K1R_FSTAMPS)
+#if defined(SNAPPY_K1R_LSTAMPS)
 #define MSTAMP(var)                                                                         \
     do {                                                                                    \
         __builtin_amdgcn_sched_barrier(0);                                                  \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory");        \
         __builtin_amdgcn_sched_barrier(0);                                                  \
     } while (0)
+#define LSTAMP(var) MSTAMP(var)
+#define LSEG(i, a, b) seg[i] += (b) - (a)
 #else
-#define MSTAMP(var) do { } while (0)
-#endif
-#ifdef SNAPPY_K1R_STAMPS
-#define STAMP(var) MSTAMP(var)
-#define SEG(i, a, b) seg[i] += (b) - (a)
-#else
-#define STAMP(var) do { } while (0)
-#define SEG(i, a, b) do { } while (0)
+#define LSTAMP(var) do { } while (0)
+#define LSEG(i, a, b) do { } while (0)
 #endif
 
 template <bool BIG>
-__device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit, uint32_t hdr_mode,
-                                         uint64_t header_value, uint2 *__restrict__ tokens, uint32_t tok_cap,
-                                         uint32_t *__restrict__ ntok_out, uint32_t *__restrict__ sizes)
+__device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
+                                         uint2 *__restrict__ tokens, uint32_t tok_cap,
+                                         uint32_t *__restrict__ ntok_out)
 {
     constexpr int W = SNAPPY_K1R_WINDOW;
-    constexpr uint32_t NREG = BIG ? kRegsBig : kRegs;
-    (void)NREG;
-    (void)hdr_mode;
-    (void)header_value;
-#ifndef SNAPPY_K1R_TABLE16
-    // 12 KiB: u16 positions + u8 tags: 12 units/CU (the VGPR limit) instead of
-    // 10 with u32 entries
-    __shared__ uint16_t tpos[kTable];
-    __shared__ uint8_t ttag[kTable];
+    constexpr uint32_t DMAX = SNAPPY_K1R_DMAX;
+    static_assert(DMAX >= 2 && DMAX <= 16, "DMAX: 2..16 (kcap <= 15 keeps the lane masks in range)");
+    // 12 KiB: 4096 packed 3-byte records (u16 position, u8 tag) at byte 3 * slot:
+    // one unaligned ds_read_b32 fetches position | tag << 16 (bits 24..31 are
+    // the next record's), a ds_write_b16 + ds_write_b8_d16_hi store one; the
+    // highest lane wins a record shared within one instruction pair
+    // (tools/micro/lds_packed3.hip).  12 units/CU (with the VGPR limit).
+    __shared__ __attribute__((aligned(16))) uint8_t tbl_[3 * kTable + 4];
+    auto *const tbl = (__attribute__((address_space(3))) uint8_t *)tbl_;
 #define TAG_OF(v) (((v) * kTagMul) >> 24)
-#define TBL_READ(h) ((uint32_t)tpos[h] | ((uint32_t)ttag[h] << 16))
-#define TBL_WRITE(s, word) do { const uint32_t _w = (word); tpos[s] = (uint16_t)_w; ttag[s] = (uint8_t)(_w >> 16); } while (0)
-#else
-    // 16 KiB: u32 entries, position | 16-bit tag << 16
-    __shared__ uint32_t table[kTable];
-#define TAG_OF(v) (((v) * kTagMul) >> 16)
-#define TBL_READ(h) table[h]
-#define TBL_WRITE(s, word) table[s] = (word)
-#endif
+#define TBL_READ3(adr) (*(__attribute__((address_space(3))) u32u *)(tbl + (adr)))
+#define TBL_WRITE3(adr, word)                                                                       \
+    do {                                                                                           \
+        const uint32_t _a = (adr), _w = (word);                                                    \
+        *(__attribute__((address_space(3))) u16u *)(tbl + _a) = (uint16_t)_w;                       \
+        tbl[_a + 2] = (uint8_t)(_w >> 16);                                                         \
+    } while (0)
+#define TBL_READ(h) TBL_READ3(3 * (h))
+#define TBL_WRITE(s, word) TBL_WRITE3(3 * (s), word)
+// tag bits 16..23 of an entry against those of a hash|tag word
+#define TAG_EQ(e, w) ((((e) ^ (w)) & 0xFF0000u) == 0)
     const uint32_t lane = threadIdx.x;
     const uint32_t u = blockIdx.x;
     const uint64_t base = (uint64_t)u * unit;
@@ -582,16 +534,14 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     const uint8_t *src = in + base;
 #ifdef SNAPPY_K1R_STATS
     const uint64_t t_start = clock64();
+    (void)t_start;
 #endif
 
-    // unit -> VGPRs (halo layout), big-endian, zero past the end
+    // unit -> registers, big-endian dwords, zero past the end
     v32 g0, g1, g2, g3;
-    v3u g4;
     const bool aligned = ((reinterpret_cast<uintptr_t>(src) & 3) == 0);
-    // big-endian dword (halo layout) of register i, zero past the end
     auto load_word = [&](uint32_t i) -> uint32_t {
-        const uint32_t d = 63 * i + lane;  // lane 63: the next register's first dword
-        const uint32_t b = 4 * d;
+        const uint32_t b = 4 * (64 * i + lane);
         uint32_t w = 0;
         if (b + 4 <= L && aligned) {
             w = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(src + b));
@@ -607,142 +557,27 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         if (i < 32) g0[i] = w;
         else if (i < 64) g1[i - 32] = w;
         else if (i < 96) g2[i - 64] = w;
-        else if (i < 128) g3[i - 96] = w;
-        else g4[i - 128] = w;
+        else g3[i - 96] = w;
     }
     if constexpr (BIG) {
 #define K1R_AW(k) asm volatile("v_accvgpr_write_b32 a" #k ", %0" ::"v"(load_word(kRegs + (k))) : "a" #k)
-        K1R_AW(0);
-        K1R_AW(1);
-        K1R_AW(2);
-        K1R_AW(3);
-        K1R_AW(4);
-        K1R_AW(5);
-        K1R_AW(6);
-        K1R_AW(7);
-        K1R_AW(8);
-        K1R_AW(9);
-        K1R_AW(10);
-        K1R_AW(11);
-        K1R_AW(12);
-        K1R_AW(13);
-        K1R_AW(14);
-        K1R_AW(15);
-        K1R_AW(16);
-        K1R_AW(17);
-        K1R_AW(18);
-        K1R_AW(19);
-        K1R_AW(20);
-        K1R_AW(21);
-        K1R_AW(22);
-        K1R_AW(23);
-        K1R_AW(24);
-        K1R_AW(25);
-        K1R_AW(26);
-        K1R_AW(27);
-        K1R_AW(28);
-        K1R_AW(29);
-        K1R_AW(30);
-        K1R_AW(31);
-        K1R_AW(32);
-        K1R_AW(33);
-        K1R_AW(34);
-        K1R_AW(35);
-        K1R_AW(36);
-        K1R_AW(37);
-        K1R_AW(38);
-        K1R_AW(39);
-        K1R_AW(40);
-        K1R_AW(41);
-        K1R_AW(42);
-        K1R_AW(43);
-        K1R_AW(44);
-        K1R_AW(45);
-        K1R_AW(46);
-        K1R_AW(47);
-        K1R_AW(48);
-        K1R_AW(49);
-        K1R_AW(50);
-        K1R_AW(51);
-        K1R_AW(52);
-        K1R_AW(53);
-        K1R_AW(54);
-        K1R_AW(55);
-        K1R_AW(56);
-        K1R_AW(57);
-        K1R_AW(58);
-        K1R_AW(59);
-        K1R_AW(60);
-        K1R_AW(61);
-        K1R_AW(62);
-        K1R_AW(63);
-        K1R_AW(64);
-        K1R_AW(65);
-        K1R_AW(66);
-        K1R_AW(67);
-        K1R_AW(68);
-        K1R_AW(69);
-        K1R_AW(70);
-        K1R_AW(71);
-        K1R_AW(72);
-        K1R_AW(73);
-        K1R_AW(74);
-        K1R_AW(75);
-        K1R_AW(76);
-        K1R_AW(77);
-        K1R_AW(78);
-        K1R_AW(79);
-        K1R_AW(80);
-        K1R_AW(81);
-        K1R_AW(82);
-        K1R_AW(83);
-        K1R_AW(84);
-        K1R_AW(85);
-        K1R_AW(86);
-        K1R_AW(87);
-        K1R_AW(88);
-        K1R_AW(89);
-        K1R_AW(90);
-        K1R_AW(91);
-        K1R_AW(92);
-        K1R_AW(93);
-        K1R_AW(94);
-        K1R_AW(95);
-        K1R_AW(96);
-        K1R_AW(97);
-        K1R_AW(98);
-        K1R_AW(99);
-        K1R_AW(100);
-        K1R_AW(101);
-        K1R_AW(102);
-        K1R_AW(103);
-        K1R_AW(104);
-        K1R_AW(105);
-        K1R_AW(106);
-        K1R_AW(107);
-        K1R_AW(108);
-        K1R_AW(109);
-        K1R_AW(110);
-        K1R_AW(111);
-        K1R_AW(112);
-        K1R_AW(113);
-        K1R_AW(114);
-        K1R_AW(115);
-        K1R_AW(116);
-        K1R_AW(117);
-        K1R_AW(118);
-        K1R_AW(119);
-        K1R_AW(120);
-        K1R_AW(121);
-        K1R_AW(122);
-        K1R_AW(123);
-        K1R_AW(124);
-        K1R_AW(125);
-        K1R_AW(126);
-        K1R_AW(127);
-        K1R_AW(128);
-        K1R_AW(129);
-        K1R_AW(130);  // spare (zeros): gathers may name register R + 1 = 261 without a bounds test
+#define K1R_AW8(k) K1R_AW(k##0); K1R_AW(k##1); K1R_AW(k##2); K1R_AW(k##3); K1R_AW(k##4); K1R_AW(k##5); K1R_AW(k##6); K1R_AW(k##7)
+        K1R_AW(0); K1R_AW(1); K1R_AW(2); K1R_AW(3); K1R_AW(4); K1R_AW(5); K1R_AW(6); K1R_AW(7);
+        K1R_AW(8); K1R_AW(9);
+        K1R_AW8(1); K1R_AW(18); K1R_AW(19);
+        K1R_AW8(2); K1R_AW(28); K1R_AW(29);
+        K1R_AW8(3); K1R_AW(38); K1R_AW(39);
+        K1R_AW8(4); K1R_AW(48); K1R_AW(49);
+        K1R_AW8(5); K1R_AW(58); K1R_AW(59);
+        K1R_AW8(6); K1R_AW(68); K1R_AW(69);
+        K1R_AW8(7); K1R_AW(78); K1R_AW(79);
+        K1R_AW8(8); K1R_AW(88); K1R_AW(89);
+        K1R_AW8(9); K1R_AW(98); K1R_AW(99);
+        K1R_AW8(10); K1R_AW(108); K1R_AW(109);
+        K1R_AW8(11); K1R_AW(118); K1R_AW(119);
+        K1R_AW(120); K1R_AW(121); K1R_AW(122); K1R_AW(123); K1R_AW(124); K1R_AW(125); K1R_AW(126); K1R_AW(127);
+        K1R_AW(128);  // spare: load_word(256) is zero for 65,536-byte units
+#undef K1R_AW8
 #undef K1R_AW
     }
 
@@ -751,7 +586,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     const uint32_t shift = 32 - lg;
 
     // never-set slots mean position 0 (snappy_compression.c:259-265): tag of BE32(0)
-    const uint32_t cur0 = BE32_REG(0);
+    const uint32_t cur0 = __builtin_amdgcn_readfirstlane(REG_OF(0));
     const uint32_t init = TAG_OF(cur0) << 16;
     for (uint32_t i = lane; i < kTable; i += 64) TBL_WRITE(i, init);
     __syncthreads();
@@ -760,94 +595,54 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     uint32_t tka = 0, tkb = 0;  // 64 pending tokens, lane t holds token t
     uint32_t nt = 0;
 
-    // position window: lane l <-> position q0 + l
-    uint32_t q0 = 0xFFFFFFFFu, hv = 0, bv = 0, dv = 0, d0 = 0xFFFF0000u;  // d0: forces the first refresh
-// dv: lane l <- dword d0 + l (256 bytes, refreshed when q0 / 4 leaves
-// [d0, d0 + 34], which keeps both the position window and a match's 16
-// verification dwords inside it); position window: lane l <- BE32 at q0 + l
-// (from dwords q0/4 + k, k = ((q0 & 3) + l) / 4 <= 16)
+    // ---- position window at q0 (see the header): dv = dwords q0/4 .. q0/4 + 63
+    uint32_t q0 = 0, d0 = 0, dv = 0, bv = 0, hv = 0;
+    uint32_t pdl1 = 0, pdc = 0, ent = 0;      // lane-space data: predecessor lane + 1, its position, entry
+    uint32_t adr = 0, word = 0;               // the lane's table record address and its insert word
+    uint64_t m_pdt = 0, m_win = 0, m_win17 = 0;
+    bool lsw = false;  // the lane-space data describe the current window
 #define WINDOW_AT(qq)                                                                              \
     do {                                                                                           \
         q0 = (qq);                                                                                 \
-        if ((q0 >> 2) - d0 > 34) {                                                                 \
-            d0 = q0 >> 2;                                                                          \
-            dv = DW_LANES(d0);                                                                     \
-        }                                                                                          \
-        const uint32_t _k = (q0 >> 2) - d0 + (((q0 & 3) + lane) >> 2);                            \
+        d0 = q0 >> 2;                                                                              \
+        dv = DW_LANES(d0);                                                                         \
+        const uint32_t _k = ((q0 & 3) + lane) >> 2;                                                \
         const uint32_t _a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_k << 2), (int)dv);       \
         const uint32_t _b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_k + 1) << 2), (int)dv); \
-        const uint32_t _s = 8 * ((q0 + lane) & 3);                                                 \
-        bv = funnel_be(_a, _b, _s);                                                                \
+        bv = funnel_bytes(_a, _b, perm_sel((q0 + lane) & 3));                                     \
         hv = ((bv * kMul) >> shift) | (TAG_OF(bv) << 16);                                          \
     } while (0)
-
-// lanes 0..15 <- BE32 at pp + 4*lane from the dword window
-#define PV_LANES16(pp)                                                                             \
-    ({                                                                                             \
-        const uint32_t _pp = (pp);                                                                 \
-        const uint32_t _kp = (_pp >> 2) - d0 + (lane & 15);                                        \
-        const uint32_t _pa = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_kp << 2), (int)dv);     \
-        const uint32_t _pb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_kp + 1) << 2), (int)dv); \
-        const uint32_t _ps = 8 * (_pp & 3);                                                        \
-        funnel_be(_pa, _pb, _ps);                                                                  \
-    })
-
-#ifdef SNAPPY_K1R_STATS
-    const uint64_t t_loop = clock64();
-    uint32_t n_probe = 0, n_match = 0, n_round = 0;
-    uint64_t t_match = 0;
-#endif
-#if defined(SNAPPY_K1R_STAMPS) || defined(SNAPPY_K1R_MSTAMPS) || defined(SNAPPY_K1R_FSTAMPS)
-    uint64_t seg[6] = {0, 0, 0, 0, 0, 0};
-    uint64_t s0, s1, s2, s3, s4, s5;
-#endif
-    // ---- lane-space rounds (step-1 probes, the text regime): lane l of the
-    // position window IS probe position q0 + l, so a round needs no gather of
-    // hashes.  Lane l's candidate is the table entry (read after the previous
-    // round's inserts) unless a lane in [lane0 - 1, l) has the same hash: the
-    // misses of this round insert exactly those positions (p - 1, p, ...), so
-    // the nearest such lane is then the candidate.  Same-hash distances up to
-    // DMAX are found once per window (DPP wave_shr chain), so a round can
-    // speculate DMAX probes with no conflict stops.
-    constexpr uint32_t DMAX = SNAPPY_K1R_DMAX;
-    uint32_t pd = 0, pdc = 0, pdt = 0, ent = 0, lmax = 0;
-    bool lsw = false;  // pd/pdc/pdt/ent describe the current window
 #define WINDOW_LS(qq)                                                                              \
     do {                                                                                           \
         WINDOW_AT(qq);                                                                             \
         const uint32_t _bits = same_x_bits<DMAX>((hv & 0xFFFF) + 1);                               \
-        pd = _bits ? (uint32_t)__builtin_ctz(_bits) : 0xFFFFFFFFu;                                 \
-        pdc = q0 + lane - pd;                                                                      \
-        const uint32_t _hp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - pd) & 63) << 2), (int)hv); \
-        pdt = _hp == hv ? 1u : 0u;                                                                 \
-        /* probe lanes keep the verification's dwords inside dv: pf / 4 <= d0 + 47 */             \
-        lmax = 4 * d0 + 191 - q0;                                                                  \
-        lmax = lmax < 62 ? lmax : 62;                                                              \
-        ent = TBL_READ(hv & 0xFFFF);                                                               \
+        const uint32_t _pd = _bits ? (uint32_t)__builtin_ctz(_bits) : 0u;                          \
+        pdl1 = _bits ? lane - _pd + 1 : 0xFFFFFF00u; /* signed: below every lane0 */             \
+        pdc = q0 + lane - _pd;                                                                     \
+        const uint32_t _hp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - _pd) & 63) << 2), (int)hv); \
+        m_pdt = __ballot(_hp == hv);                                                               \
+        /* probe lanes: <= 62 and not past is_block_end (L - p >= 16, 17 at skip 64) */           \
+        const int32_t _w16 = (int32_t)(L - 16 - q0), _w17 = (int32_t)(L - 17 - q0);              \
+        m_win = __ballot((int32_t)lane <= _w16 && lane <= 62);                                     \
+        m_win17 = __ballot((int32_t)lane <= _w17 && lane <= 62);                                   \
+        adr = 3 * (hv & 0xFFFF);                                                                   \
+        word = (q0 + lane) | (hv & 0xFF0000u);                                                     \
+        ent = TBL_READ3(adr);                                                                      \
         lsw = true;                                                                                \
     } while (0)
 
     // find_copy_length :61-72 after found_match :259-265: common prefix of the
-    // bytes at pf and cand (lanes 0..15 compare 64 bytes, then 252 per pass)
-    auto match_len = [&](uint32_t pf, uint32_t cand) -> uint32_t {
-        const uint32_t y = (PV_LANES16(pf) ^ BE32_LANES16(cand)) & (uint32_t)(((int32_t)(lane - 16)) >> 31);
-        const uint64_t bad = __ballot(y != 0);
-        uint32_t len;
-        if (bad) {
-            const uint32_t m = (uint32_t)__builtin_ctzll(bad);
-            len = 4 * m + ((uint32_t)__builtin_clz(__builtin_amdgcn_readlane(y, m)) >> 3);
-        } else {
-            len = 64;
+    // bytes at pf (pf - q0 <= 62: its dwords come from dv) and cand
+    // (registers); lanes 0..15 compare 64 bytes, then 252 per pass
+    // common prefix continued from len (all bytes before it equal), 252 bytes per pass
+    auto match_len_from = [&](uint32_t pf, uint32_t cand, uint32_t len) -> uint32_t {
             for (;;) {
                 if (pf + len >= L) break;
                 const uint32_t qa = pf + len, qb = cand + len;
                 const uint32_t a0 = DW_LANES(qa >> 2), b0 = DW_LANES(qb >> 2);
-                const int nx = (int)(((lane + 1) & 63) << 2);
-                const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute(nx, (int)a0);
-                const uint32_t b1 = (uint32_t)__builtin_amdgcn_ds_bpermute(nx, (int)b0);
-                const uint32_t va = funnel_be(a0, a1, 8 * (qa & 3));
-                const uint32_t vb = funnel_be(b0, b1, 8 * (qb & 3));
-                const uint32_t yy = lane < 63 ? (va ^ vb) : 0;
+                const uint32_t va = funnel_bytes(a0, wave_shl1(a0), perm_sel(qa & 3));
+                const uint32_t vb = funnel_bytes(b0, wave_shl1(b0), perm_sel(qb & 3));
+                const uint32_t yy = lane < 63 ? (va ^ vb) : 0;  // lane 63 lacks its successor
                 const uint64_t bb = __ballot(yy != 0);
                 if (bb) {
                     const uint32_t m = (uint32_t)__builtin_ctzll(bb);
@@ -856,94 +651,154 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 }
                 len += 252;
             }
-        }
         return len;
     };
+    auto match_len = [&](uint32_t pf, uint32_t cand) -> uint32_t {
+        const uint32_t kp = (pf >> 2) - d0;
+        const uint32_t pa = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((kp + lane) & 63) << 2), (int)dv);
+        const uint32_t ca = DW_LANES(cand >> 2);
+        const uint32_t pv = funnel_bytes(pa, wave_shl1(pa), perm_sel(pf & 3));
+        const uint32_t cv = funnel_bytes(ca, wave_shl1(ca), perm_sel(cand & 3));
+        const uint32_t y = pv ^ cv;
+        const uint64_t bad = __ballot(y != 0) & 0xFFFFull;
+        if (bad) {
+            const uint32_t m = (uint32_t)__builtin_ctzll(bad);
+            return 4 * m + ((uint32_t)__builtin_clz(__builtin_amdgcn_readlane(y, m)) >> 3);
+        }
+        return match_len_from(pf, cand, 64);
+    };
+    // emit_copy :323-329 as a token (the caller inserts pf into the table)
+    auto put_token = [&](uint32_t pf, uint32_t len, uint32_t off) {
+        tka = (uint32_t)amdgcn_writelane((int)(pf | (len << 16)), (int)(nt & 63), (int)tka);
+        tkb = (uint32_t)amdgcn_writelane((int)off, (int)(nt & 63), (int)tkb);
+        nt++;
+        if ((nt & 63) == 0) tok[nt - 64 + lane] = make_uint2(tka, tkb);
+    };
 
+#ifdef SNAPPY_K1R_STATS
+    const uint64_t t_loop = clock64();
+    uint32_t n_probe = 0, n_match = 0, n_round = 0;
+#endif
+#if defined(SNAPPY_K1R_LSTAMPS)
+    uint64_t seg[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t s0, s1, s2, s3, s4, s5;
+#endif
     uint32_t p = 1, skip = 33;
     while (!(L - p < (skip >> 5) + 15)) {  // is_block_end :229-232
 #ifdef SNAPPY_K1R_STATS
         n_round++;
 #endif
-#ifndef SNAPPY_K1R_LEGACY
         if (skip <= 64 - SNAPPY_K1R_LSMIN) {
-            uint32_t lane0 = p - q0;
-            if (!lsw || p - 1 < q0 || lane0 + SNAPPY_K1R_RMIN > lmax) {
-                WINDOW_LS(p - 1);
-                lane0 = 1;
-            }
-            // last speculative offset k: step 1 ((skip + k - 1) >> 5 == 1 before it),
-            // predecessors within DMAX, inside the window, not past is_block_end
-            uint32_t kmax = 64 - skip;
-            kmax = kmax < DMAX - 1 ? kmax : DMAX - 1;
-            kmax = kmax < lmax - lane0 ? kmax : lmax - lane0;
-            kmax = kmax < L - p - 16 ? kmax : L - p - 16;
-            if (skip + kmax == 64 && L - p - kmax < 17) kmax--;
-            const uint32_t k = lane - lane0;
-            // lane0's own lookup precedes every insert of the round
-            const bool inr = pd <= k + 1 && k != 0;
-            const uint32_t cand = inr ? pdc : (ent & 0xFFFF);
-            const bool hit = inr ? (pdt != 0) : (((ent ^ hv) >> 16) == 0);
-            const uint64_t hm = __ballot(k <= kmax && hit);
-            uint32_t lo = lane0 - 1, hi, np;
-            if (hm) {
-                const uint32_t f = (uint32_t)__builtin_ctzll(hm);
-                const uint32_t pf = q0 + f;
-                const uint32_t c = __builtin_amdgcn_readlane(cand, f);
-                uint32_t len = match_len(pf, c);
-                hi = f;
-#ifdef SNAPPY_K1R_STATS
-                n_probe += f - lane0 + 1;
-#endif
-                if (len >= 4) {  // emit_copy :323-329 (the table insert of pf is lane f's)
-                    if (len > L - pf) len = L - pf;
-#ifdef SNAPPY_K1R_STATS
-                    n_match++;
-#endif
-                    tka = (uint32_t)amdgcn_writelane((int)(pf | (len << 16)), (int)(nt & 63), (int)tka);
-                    tkb = (uint32_t)amdgcn_writelane((int)(pf - c), (int)(nt & 63), (int)tkb);
-                    nt++;
-                    if ((nt & 63) == 0) tok[nt - 64 + lane] = make_uint2(tka, tkb);
-                    if (f == lane0) lo = lane0;  // a first-probe match inserts no p - 1
-                    np = pf + len;
-                    skip = 32;
-                } else {  // tag collision: a miss (append_literal :283-287 steps by skip >> 5)
-                    np = pf + ((skip + f - lane0) >> 5);
-                    skip += f - lane0 + 1;
+            // ---------------- lane-space rounds until a step > 1 or the block end
+            do {
+                LSTAMP(s0);
+                uint32_t lane0 = p - q0;
+                if (!lsw || lane0 + SNAPPY_K1R_RMIN > 62) {
+                    WINDOW_LS(p - 1);
+                    lane0 = 1;
                 }
-            } else {
-                const uint32_t f = lane0 + kmax + 1;
-                hi = f - 1;
-                np = q0 + f - 1 + ((skip + kmax) >> 5);  // the last probe steps by 2 at skip 64
-                skip += kmax + 1;
+                // probe k = lane - lane0 for k <= kcap: step 1 before it ((skip + k - 1) >> 5 == 1),
+                // predecessors within DMAX; inside the window and before is_block_end (m_win);
+                // the probe at skip + k == 64 needs L - p_k >= 17
+                uint64_t valid;
+                if (skip <= 64 - DMAX) {
+                    valid = (((1ull << DMAX) - 1) << lane0) & m_win;
+                } else {
+                    const uint32_t kcap = 64 - skip;
+                    valid = ((2ull << kcap) - 1) << lane0;
+                    if (lane0 + kcap < 64) valid &= ~((1ull << (lane0 + kcap)) & ~m_win17);
+                    valid &= m_win;
+                }
+                // lane l > lane0 takes the in-round candidate when its nearest same-hash lane is >= lane0 - 1
+                const bool inr = (int32_t)pdl1 >= (int32_t)lane0 && lane > lane0;
+                const uint64_t m_inr = __ballot(inr);
+                const uint64_t m_tag = __ballot(TAG_EQ(ent, word));
+                const uint64_t hm = ((m_inr & m_pdt) | (m_tag & ~m_inr)) & valid;
+                const uint32_t candv = inr ? pdc : ent;
+                LSTAMP(s1);
+                LSEG(0, s0, s1);
+                uint32_t np;
+                if (hm) {
+                    const uint32_t f = (uint32_t)__builtin_ctzll(hm);
+                    const uint32_t pf = q0 + f;
+                    const uint32_t c = __builtin_amdgcn_readlane(candv, f) & 0xFFFF;
+                    // find_copy_length :61-72 after found_match :259-265: lanes 0..15
+                    // compare the 64 bytes at pf (dwords from dv) and c (registers)
+                    const uint32_t pa = (uint32_t)__builtin_amdgcn_ds_bpermute(
+                        (int)(((((pf >> 2) - d0) + lane) & 63) << 2), (int)dv);
+                    const uint32_t ca = DW_LANES(c >> 2);
+                    __builtin_amdgcn_sched_barrier(0);
+                    // the inserts known before the verdict: misses p_k - 1, p_k and the
+                    // probe at f (miss or match) -- all of [lane0 - 1, f] unless f is the
+                    // first probe (its p - 1 is inserted only if it misses)
+                    const uint32_t lo0 = f > lane0 ? lane0 - 1 : lane0;
+                    if (lane - lo0 <= f - lo0) TBL_WRITE3(adr, word);
+                    ent = TBL_READ3(adr);
+                    LSTAMP(s2);
+                    LSEG(1, s1, s2);
+                    const uint32_t pv = funnel_bytes(pa, wave_shl1(pa), perm_sel(pf & 3));
+                    const uint32_t cv = funnel_bytes(ca, wave_shl1(ca), perm_sel(c & 3));
+                    const uint32_t y = pv ^ cv;
+                    const uint64_t bad = __ballot(y != 0) & 0xFFFFull;
+                    uint32_t len;
+                    if (bad) {
+                        const uint32_t m = (uint32_t)__builtin_ctzll(bad);
+                        len = 4 * m + ((uint32_t)__builtin_clz(__builtin_amdgcn_readlane(y, m)) >> 3);
+                    } else {
+                        len = match_len_from(pf, c, 64);
+                    }
+                    LSTAMP(s3);
+                    LSEG(2, s2, s3);
 #ifdef SNAPPY_K1R_STATS
-                n_probe += kmax + 1;
+                    n_probe += f - lane0 + 1;
 #endif
-            }
-            // update_hash_table :303-307 for the misses (p_k - 1 and p_k) and the
-            // match's own slot: every position of [lo, hi] once, the highest lane
-            // (latest position) winning a shared slot
-            if (lane - lo <= hi - lo) TBL_WRITE(hv & 0xFFFF, (q0 + lane) | (hv & 0xFFFF0000u));
-            ent = TBL_READ(hv & 0xFFFF);
-            p = np;
+                    if (len >= 4) {
+                        if (len > L - pf) len = L - pf;  // the compare never runs past the block
+#ifdef SNAPPY_K1R_STATS
+                        n_match++;
+#endif
+                        put_token(pf, len, pf - c);
+                        np = pf + len;
+                        skip = 32;
+                    } else {  // tag collision: a miss (append_literal :283-287 steps by skip >> 5)
+                        if (f == lane0) {  // its p - 1, then p again (the later write wins)
+                            if (lane - (lane0 - 1) <= 1) TBL_WRITE3(adr, word);
+                            ent = TBL_READ3(adr);
+                        }
+                        np = pf + ((skip + f - lane0) >> 5);
+                        skip += f - lane0 + 1;
+                    }
+                } else {
+                    const uint32_t nk = (uint32_t)__builtin_popcountll(valid);  // lanes lane0 .. lane0 + nk - 1
+                    // update_hash_table :303-307: p_k - 1 and p_k of every miss, lane order
+                    if (lane - (lane0 - 1) <= nk) TBL_WRITE3(adr, word);
+                    ent = TBL_READ3(adr);
+                    np = q0 + lane0 + nk - 1 + ((skip + nk - 1) >> 5);  // the last probe steps by 2 at skip 64
+                    skip += nk;
+#ifdef SNAPPY_K1R_STATS
+                    n_probe += nk;
+#endif
+                }
+                p = np;
+                LSTAMP(s4);
+                LSEG(3, s3, s4);
+                LSEG(4, s0, s4);
+#ifdef SNAPPY_K1R_STATS
+                n_round++;
+#endif
+            } while (skip <= 64 - SNAPPY_K1R_LSMIN && !(L - p < (skip >> 5) + 15));
+#ifdef SNAPPY_K1R_STATS
+            n_round--;
+#endif
             continue;
         }
+        // ---------------- W-probe round (steps > 1)
         lsw = false;
-#endif
-        STAMP(s0);
         if (p - 1 < q0 || p + 12 > q0 + 64) WINDOW_AT(p - 1);
-        STAMP(s1);
-        SEG(0, s0, s1);
-        // ---- speculative window: lane k = k-th probe if all earlier miss
+        // lane k = k-th probe if all earlier miss, at its closed-form position
         const uint32_t sk = skip + lane;
-        uint32_t pk, bend;  // probe position, is_block_end bound (skip >> 5) + 15
-        if (skip <= 64 - W) {  // every speculative lane steps by 1 (after a match: skip = 32)
-            pk = p + lane;
-            bend = 16;
-        } else {
-            pk = p + skipsum(sk) - skipsum(skip);
-            bend = (sk >> 5) + 15;
-        }
+        const uint32_t pk = p + skipsum(sk) - skipsum(skip);
+        const uint32_t bend = (sk >> 5) + 15;
         // invalid: lane >= W, block end (is_block_end), or past the window
         const uint32_t inval = (uint32_t)(((int32_t)(W - 1 - lane)) >> 31) |
                                (uint32_t)(((int32_t)(L - pk) - (int32_t)bend) >> 31) |
@@ -952,138 +807,37 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         const uint32_t hvp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ik << 2), (int)hv);
         const uint32_t hvq = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((ik - 1) << 2), (int)hv);
         const uint32_t h = hvp & 0xFFFF, a = hvq & 0xFFFF;
-        STAMP(s2);
-        SEG(1, s1, s2);
-        const uint32_t ent = TBL_READ(h);
-#ifdef SNAPPY_K1R_EARLY_READ
-        __builtin_amdgcn_sched_barrier(0);  // issue the table read before the conflict math
-#endif
+        const uint32_t e = TBL_READ(h);
         // previous lane stepped by 1 iff its skip counter was 32..63
         const uint32_t notdup = ~eqm(((sk - 1) >> 5) ^ 1);
         const uint32_t conflict = tconf<W>(h, a, notdup) & ~eqm(lane);
-        const uint32_t hit = eqm((ent ^ hvp) >> 16);
+        const uint32_t hit = TAG_EQ(e, hvp) ? 0xFFFFFFFFu : 0u;
         const uint64_t stop = __ballot((inval | conflict | hit) != 0);
         const uint32_t f = (uint32_t)__builtin_ctzll(stop);
-        STAMP(s3);
-        SEG(2, s2, s3);
         // lanes before f are exact misses: update_hash_table :303-307
         if (lane < f) {
             TBL_WRITE(a, (pk - 1) | (hvq & 0xFFFF0000u));
             TBL_WRITE(h, pk | (hvp & 0xFFFF0000u));
         }
         const uint64_t hits = __ballot((hit & ~(inval | conflict)) != 0);
-        STAMP(s4);
-        SEG(3, s3, s4);
 #ifdef SNAPPY_K1R_STATS
         n_probe += f + ((hits >> f) & 1);
 #endif
         uint32_t next_f = f;  // probes consumed if no match
         if ((hits >> f) & 1) {
-#ifdef SNAPPY_K1R_STATS
-            const uint64_t tm0 = clock64();
-#endif
-#if defined(SNAPPY_K1R_MSTAMPS) || defined(SNAPPY_K1R_FSTAMPS)
-            uint64_t m0;
-            MSTAMP(m0);
-#endif
-#ifdef SNAPPY_K1R_MSTAMPS
-            uint64_t m1, m2, m3;
-#endif
             const uint32_t pf = __builtin_amdgcn_readlane(pk, f);
-            const uint32_t cand = __builtin_amdgcn_readlane(ent, f) & 0xFFFF;
+            const uint32_t cand = __builtin_amdgcn_readlane(e, f) & 0xFFFF;
             const uint32_t hf = __builtin_amdgcn_readlane(hvp, f);
-            // lanes 0..15 compare BE32 at pf + 4j and cand + 4j: verification
-            // (first 4 bytes) and find_copy_length :61-72 up to 64 bytes at once
-            // pf side from the dword window (pf <= q0 + 52 and q0 / 4 - d0 <= 34: index <= 63)
-#ifdef SNAPPY_K1R_FSTAMPS
-            // fine-grained attribution of the verification gather (stamps drain lgkm)
-            uint64_t fa, fb, fc, mf1;
-            asm volatile("" ::"s"(pf), "s"(cand), "s"(hf));
-            MSTAMP(fa);
-            const uint32_t _q = cand, _d0 = _q >> 2, _R = HALO_R(_d0);
-            const uint32_t _e = _d0 + (lane & 15);
-            const uint32_t _re = HALO_R(_e) - _R;
-            const uint32_t _le = _e - 63 * (_R + _re);
-            const uint32_t _r0 = REG_OF(_R), _r1 = REG_OF(_R + 1);
-            asm volatile("" ::"v"(_r0), "v"(_r1));
-            MSTAMP(fb);
-            const uint32_t pvv = PV_LANES16(pf);
-            const uint32_t _x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)_r0);
-            const uint32_t _x1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_le + 1) << 2), (int)_r0);
-            const uint32_t _y0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_le << 2), (int)_r1);
-            const uint32_t _y1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_le + 1) << 2), (int)_r1);
-            asm volatile("" ::"v"(_x0), "v"(_x1), "v"(_y0), "v"(_y1), "v"(pvv));
-            MSTAMP(fc);
-            const uint32_t _hi = _re ? _y0 : _x0, _lo = _re ? _y1 : _x1;
-            const uint32_t _s = 8 * (_q & 3);
-            const uint32_t cv = funnel_be(_hi, _lo, _s);
-            const uint32_t y = (pvv ^ cv) & (uint32_t)(((int32_t)(lane - 16)) >> 31);
-            const uint64_t bad = __ballot(y != 0);
-            asm volatile("" ::"s"(bad));
-            MSTAMP(mf1);
-            seg[0] += fa - m0;
-            seg[1] += fb - fa;
-            seg[2] += fc - fb;
-            seg[3] += mf1 - fc;
-#else
-            const uint32_t y = (PV_LANES16(pf) ^ BE32_LANES16(cand)) & (uint32_t)(((int32_t)(lane - 16)) >> 31);
-            const uint64_t bad = __ballot(y != 0);
-#endif
-#ifdef SNAPPY_K1R_MSTAMPS
-            MSTAMP(m1);
-            seg[0] += m1 - m0;
-#endif
-            uint32_t len;
-            if (bad) {
-                const uint32_t m = (uint32_t)__builtin_ctzll(bad);
-                len = 4 * m + ((uint32_t)__builtin_clz(__builtin_amdgcn_readlane(y, m)) >> 3);
-            } else {
-                len = 64;  // 252 bytes per wave pass from here
-                for (;;) {
-                    if (pf + len >= L) break;
-                    const uint32_t qa = pf + len, qb = cand + len;
-                    const uint32_t a0 = DW_LANES(qa >> 2), b0 = DW_LANES(qb >> 2);
-                    const int nx = (int)(((lane + 1) & 63) << 2);
-                    const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute(nx, (int)a0);
-                    const uint32_t b1 = (uint32_t)__builtin_amdgcn_ds_bpermute(nx, (int)b0);
-                    const uint32_t sa = 8 * (qa & 3), sb = 8 * (qb & 3);
-                    const uint32_t va = funnel_be(a0, a1, sa);
-                    const uint32_t vb = funnel_be(b0, b1, sb);
-                    const uint32_t yy = lane < 63 ? (va ^ vb) : 0;  // lane 63 lacks its successor
-                    const uint64_t bb = __ballot(yy != 0);
-                    if (bb) {
-                        const uint32_t m = (uint32_t)__builtin_ctzll(bb);
-                        len += 4 * m + ((uint32_t)__builtin_clz(__builtin_amdgcn_readlane(yy, m)) >> 3);
-                        break;
-                    }
-                    len += 252;
-                }
-            }
-#ifdef SNAPPY_K1R_MSTAMPS
-            MSTAMP(m2);
-            seg[1] += m2 - m1;
-#endif
+            uint32_t len = match_len(pf, cand);
             if (len >= 4) {  // verified: found_match :259-265
-                if (len > L - pf) len = L - pf;  // the compare never runs past the block
+                if (len > L - pf) len = L - pf;
 #ifdef SNAPPY_K1R_STATS
                 n_match++;
 #endif
-                const uint32_t off = pf - cand;
-                // token t goes to lane t & 63 of (tka, tkb)
-                tka = (uint32_t)amdgcn_writelane((int)(pf | (len << 16)), (int)(nt & 63), (int)tka);
-                tkb = (uint32_t)amdgcn_writelane((int)off, (int)(nt & 63), (int)tkb);
-                nt++;
-                if ((nt & 63) == 0) tok[nt - 64 + lane] = make_uint2(tka, tkb);
+                put_token(pf, len, pf - cand);
                 TBL_WRITE(hf & 0xFFFF, pf | (hf & 0xFFFF0000u));  // emit_copy :328
                 skip = 32;
                 p = pf + len;
-#ifdef SNAPPY_K1R_MSTAMPS
-                MSTAMP(m3);
-                seg[2] += m3 - m2;
-#endif
-#ifdef SNAPPY_K1R_STATS
-                t_match += clock64() - tm0;
-#endif
                 continue;
             }
             // tag collision: lane f is a miss as well
@@ -1096,29 +850,27 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         // edge or the block end and is retried exactly as the next lane 0
         p = skip + next_f <= 64 ? p + next_f : p + skipsum(skip + next_f) - skipsum(skip);
         skip += next_f;
-        STAMP(s5);
-        SEG(4, s4, s5);
     }
 #undef WINDOW_AT
 #undef WINDOW_LS
-#undef PV_LANES16
 #undef TAG_OF
 #undef TBL_READ
 #undef TBL_WRITE
-    (void)sizes;
+#undef TBL_READ3
+#undef TBL_WRITE3
+#undef TAG_EQ
     if (lane < (nt & 63)) tok[(nt & ~63u) + lane] = make_uint2(tka, tkb);
     if (lane == 0) ntok_out[u] = nt;
 #ifdef SNAPPY_K1R_STATS
     if (lane == 0) {
         uint64_t *st = reinterpret_cast<uint64_t *>(tokens + (uint64_t)gridDim.x * tok_cap) + 4 * (uint64_t)u;
         st[0] = clock64() - t_loop;
-#if defined(SNAPPY_K1R_STAMPS) || defined(SNAPPY_K1R_MSTAMPS) || defined(SNAPPY_K1R_FSTAMPS)
-        t_match = seg[0] | (seg[1] << 16 << 16);
+#if defined(SNAPPY_K1R_LSTAMPS)
+        st[1] = seg[0] | (seg[1] << 32);
         st[3] = seg[2] | (seg[3] << 32);
         st[2] = seg[4];
-#endif
-        st[1] = t_match;
-#if !defined(SNAPPY_K1R_STAMPS) && !defined(SNAPPY_K1R_MSTAMPS) && !defined(SNAPPY_K1R_FSTAMPS)
+#else
+        st[1] = 0;
         st[2] = n_probe | ((uint64_t)n_round << 32);
         st[3] = n_match;
 #endif
@@ -1132,18 +884,24 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
                                                           uint32_t *__restrict__ ntok_out,
                                                           uint32_t *__restrict__ sizes)
 {
-    k1r_body<false>(in, n, unit, hdr_mode, header_value, tokens, tok_cap, ntok_out, sizes);
+    (void)hdr_mode;
+    (void)header_value;
+    (void)sizes;
+    k1r_body<false>(in, n, unit, tokens, tok_cap, ntok_out);
 }
 
-// 65,536-byte blocks (the reference's MAX_BLOCK_SIZE): unit in 131 VGPRs +
-// 130 AGPRs, one wave per SIMD
+// 65,536-byte blocks (the reference's MAX_BLOCK_SIZE): unit in 128 VGPRs +
+// 128 AGPRs, one wave per SIMD
 __global__ __launch_bounds__(64, 1) void k1r_match_units64(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
                                                             uint32_t hdr_mode, uint64_t header_value,
                                                             uint2 *__restrict__ tokens, uint32_t tok_cap,
                                                             uint32_t *__restrict__ ntok_out,
                                                             uint32_t *__restrict__ sizes)
 {
-    k1r_body<true>(in, n, unit, hdr_mode, header_value, tokens, tok_cap, ntok_out, sizes);
+    (void)hdr_mode;
+    (void)header_value;
+    (void)sizes;
+    k1r_body<true>(in, n, unit, tokens, tok_cap, ntok_out);
 }
 
 // ---------------------------------------------------------------------------

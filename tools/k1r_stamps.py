@@ -28,7 +28,7 @@ loop = st[:, 0].astype(float)
 seg0, seg1 = (st[:, 1] & 0xFFFFFFFF).astype(float), (st[:, 1] >> 32).astype(float)
 seg2, seg3 = (st[:, 3] & 0xFFFFFFFF).astype(float), (st[:, 3] >> 32).astype(float)
 seg4 = st[:, 2].astype(float)
-rounds = 4333
+rounds = int(os.environ.get("K1R_ROUNDS", "3937"))
 names = sys.argv[2].split(",") if len(sys.argv) > 2 else ["window", "lanes+bpermute", "table+conflict+ballot", "inserts+ballot2", "match/advance"]
 tot = loop.sum()
 for nm, v in zip(names, [seg0, seg1, seg2, seg3, seg4]):

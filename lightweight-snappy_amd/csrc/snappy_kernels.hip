@@ -513,7 +513,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     // the next record's), a ds_write_b16 + ds_write_b8_d16_hi store one; the
     // highest lane wins a record shared within one instruction pair
     // (tools/micro/lds_packed3.hip).  12 units/CU (with the VGPR limit).
-    __shared__ __attribute__((aligned(16))) uint8_t tbl_[3 * kTable + 4];
+    __shared__ __attribute__((aligned(16))) uint8_t tbl_[3 * kTable + 8];
+    constexpr uint32_t kDummy = 3 * kTable + 4;  // a record nobody reads: the target of non-inserting lanes
     auto *const tbl = (__attribute__((address_space(3))) uint8_t *)tbl_;
 #define TAG_OF(v) (((v) * kTagMul) >> 24)
 #define TBL_READ3(adr) (*(__attribute__((address_space(3))) u32u *)(tbl + (adr)))
@@ -525,6 +526,11 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     } while (0)
 #define TBL_READ(h) TBL_READ3(3 * (h))
 #define TBL_WRITE(s, word) TBL_WRITE3(3 * (s), word)
+// Lanes communicate through the table: a read must see every earlier write of
+// the wave, including other lanes' (LDS executes a wave's accesses in order).
+// C++ sees no such dependence, so every write group is followed by a compiler
+// barrier that keeps later reads after it.
+#define LDS_ORDER() asm volatile("" ::: "memory")
 // tag bits 16..23 of an entry against those of a hash|tag word
 #define TAG_EQ(e, w) ((((e) ^ (w)) & 0xFF0000u) == 0)
     const uint32_t lane = threadIdx.x;
@@ -595,8 +601,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     uint32_t tka = 0, tkb = 0;  // 64 pending tokens, lane t holds token t
     uint32_t nt = 0;
 
-    // ---- position window at q0 (see the header): dv = dwords q0/4 .. q0/4 + 63
-    uint32_t q0 = 0, d0 = 0, dv = 0, bv = 0, hv = 0;
+    // ---- position window at q0 (see the header): dv = dwords q0/4 .. q0/4 + 63,
+    // rotated: dword q0/4 + i sits at lane (dr + i) % 64 (ds_bpermute wraps addr[7:2])
+    uint32_t q0 = 0, d0 = 0, dr = 0, dv = 0, bv = 0, hv = 0;
     uint32_t pdl1 = 0, pdc = 0, ent = 0;      // lane-space data: predecessor lane + 1, its position, entry
     uint32_t adr = 0, word = 0;               // the lane's table record address and its insert word
     uint64_t m_pdt = 0, m_win = 0, m_win17 = 0;
@@ -605,8 +612,12 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     do {                                                                                           \
         q0 = (qq);                                                                                 \
         d0 = q0 >> 2;                                                                              \
-        dv = DW_LANES(d0);                                                                         \
-        const uint32_t _k = ((q0 & 3) + lane) >> 2;                                                \
+        dr = d0 & 63;                                                                              \
+        {                                                                                          \
+            const uint32_t _r0 = REG_OF(d0 >> 6), _r1 = REG_OF((d0 >> 6) + 1);                     \
+            dv = lane >= dr ? _r0 : _r1;                                                           \
+        }                                                                                          \
+        const uint32_t _k = dr + (((q0 & 3) + lane) >> 2);                                         \
         const uint32_t _a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_k << 2), (int)dv);       \
         const uint32_t _b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_k + 1) << 2), (int)dv); \
         bv = funnel_bytes(_a, _b, perm_sel((q0 + lane) & 3));                                     \
@@ -654,8 +665,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         return len;
     };
     auto match_len = [&](uint32_t pf, uint32_t cand) -> uint32_t {
-        const uint32_t kp = (pf >> 2) - d0;
-        const uint32_t pa = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((kp + lane) & 63) << 2), (int)dv);
+        const uint32_t kp = (pf >> 2) - d0 + dr;
+        const uint32_t pa = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((kp + lane) << 2), (int)dv);
         const uint32_t ca = DW_LANES(cand >> 2);
         const uint32_t pv = funnel_bytes(pa, wave_shl1(pa), perm_sel(pf & 3));
         const uint32_t cv = funnel_bytes(ca, wave_shl1(ca), perm_sel(cand & 3));
@@ -710,11 +721,10 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     valid &= m_win;
                 }
                 // lane l > lane0 takes the in-round candidate when its nearest same-hash lane is >= lane0 - 1
-                const bool inr = (int32_t)pdl1 >= (int32_t)lane0 && lane > lane0;
-                const uint64_t m_inr = __ballot(inr);
+                const uint64_t m_inr = __ballot((int32_t)pdl1 >= (int32_t)lane0) & (~1ull << lane0);
                 const uint64_t m_tag = __ballot(TAG_EQ(ent, word));
-                const uint64_t hm = ((m_inr & m_pdt) | (m_tag & ~m_inr)) & valid;
-                const uint32_t candv = inr ? pdc : ent;
+                const uint64_t hm = (m_tag ^ ((m_tag ^ m_pdt) & m_inr)) & valid;
+                const uint32_t candv = __builtin_amdgcn_inverse_ballot_w64(m_inr) ? pdc : ent;
                 LSTAMP(s1);
                 LSEG(0, s0, s1);
                 uint32_t np;
@@ -725,14 +735,16 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     // find_copy_length :61-72 after found_match :259-265: lanes 0..15
                     // compare the 64 bytes at pf (dwords from dv) and c (registers)
                     const uint32_t pa = (uint32_t)__builtin_amdgcn_ds_bpermute(
-                        (int)(((((pf >> 2) - d0) + lane) & 63) << 2), (int)dv);
+                        (int)(((pf >> 2) - d0 + dr + lane) << 2), (int)dv);
                     const uint32_t ca = DW_LANES(c >> 2);
                     __builtin_amdgcn_sched_barrier(0);
                     // the inserts known before the verdict: misses p_k - 1, p_k and the
                     // probe at f (miss or match) -- all of [lane0 - 1, f] unless f is the
-                    // first probe (its p - 1 is inserted only if it misses)
+                    // first probe (its p - 1 is inserted only if it misses); other lanes
+                    // write the dummy record
                     const uint32_t lo0 = f > lane0 ? lane0 - 1 : lane0;
-                    if (lane - lo0 <= f - lo0) TBL_WRITE3(adr, word);
+                    TBL_WRITE3(lane - lo0 <= f - lo0 ? adr : kDummy, word);
+                    LDS_ORDER();
                     ent = TBL_READ3(adr);
                     LSTAMP(s2);
                     LSEG(1, s1, s2);
@@ -762,7 +774,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                         skip = 32;
                     } else {  // tag collision: a miss (append_literal :283-287 steps by skip >> 5)
                         if (f == lane0) {  // its p - 1, then p again (the later write wins)
-                            if (lane - (lane0 - 1) <= 1) TBL_WRITE3(adr, word);
+                            TBL_WRITE3(lane - (lane0 - 1) <= 1 ? adr : kDummy, word);
+                            LDS_ORDER();
                             ent = TBL_READ3(adr);
                         }
                         np = pf + ((skip + f - lane0) >> 5);
@@ -771,7 +784,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 } else {
                     const uint32_t nk = (uint32_t)__builtin_popcountll(valid);  // lanes lane0 .. lane0 + nk - 1
                     // update_hash_table :303-307: p_k - 1 and p_k of every miss, lane order
-                    if (lane - (lane0 - 1) <= nk) TBL_WRITE3(adr, word);
+                    TBL_WRITE3(lane - (lane0 - 1) <= nk ? adr : kDummy, word);
+                    LDS_ORDER();
                     ent = TBL_READ3(adr);
                     np = q0 + lane0 + nk - 1 + ((skip + nk - 1) >> 5);  // the last probe steps by 2 at skip 64
                     skip += nk;
@@ -819,6 +833,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             TBL_WRITE(a, (pk - 1) | (hvq & 0xFFFF0000u));
             TBL_WRITE(h, pk | (hvp & 0xFFFF0000u));
         }
+        LDS_ORDER();
         const uint64_t hits = __ballot((hit & ~(inval | conflict)) != 0);
 #ifdef SNAPPY_K1R_STATS
         n_probe += f + ((hits >> f) & 1);
@@ -836,6 +851,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #endif
                 put_token(pf, len, pf - cand);
                 TBL_WRITE(hf & 0xFFFF, pf | (hf & 0xFFFF0000u));  // emit_copy :328
+                LDS_ORDER();
                 skip = 32;
                 p = pf + len;
                 continue;
@@ -844,6 +860,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             const uint32_t af = __builtin_amdgcn_readlane(hvq, f);
             TBL_WRITE(af & 0xFFFF, (pf - 1) | (af & 0xFFFF0000u));
             TBL_WRITE(hf & 0xFFFF, pf | (hf & 0xFFFF0000u));
+            LDS_ORDER();
             next_f = f + 1;
         }
         // f (or f + 1) misses consumed; f stops at a conflict, the window
@@ -859,6 +876,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #undef TBL_READ3
 #undef TBL_WRITE3
 #undef TAG_EQ
+#undef LDS_ORDER
     if (lane < (nt & 63)) tok[(nt & ~63u) + lane] = make_uint2(tka, tkb);
     if (lane == 0) ntok_out[u] = nt;
 #ifdef SNAPPY_K1R_STATS

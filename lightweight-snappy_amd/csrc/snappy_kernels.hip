@@ -371,18 +371,46 @@ constexpr uint32_t kRegs = 128;  // VGPRs holding a 32 KiB unit (64 dwords each)
         _rv;                                                                                        \
     })
 
+// registers r and r + 1 of the resident unit with one s_set_gpr_idx_on region
+// (SRC0 of both moves is indexed); r + 1 = 128 of a 32 KiB unit reads v130,
+// which holds no unit data (see DW_LANES)
+#define REG_PAIR_V(r, lo, hi)                                                                        \
+    asm volatile("s_set_gpr_idx_on %2, gpr_idx(SRC0)\n\tv_mov_b32 %0, v2\n\tv_mov_b32 %1, v3\n\t"           \
+                 "s_set_gpr_idx_off"                                                                 \
+                 : "=&v"(lo), "=&v"(hi)                                                              \
+                 : "s"((uint32_t)(r)), "{v[2:33]}"(g0), "{v[34:65]}"(g1), "{v[66:97]}"(g2),              \
+                   "{v[98:129]}"(g3))
+#define REG_PAIR_A(r, lo, hi)                                                                        \
+    asm volatile("s_set_gpr_idx_on %2, gpr_idx(SRC0)\n\tv_accvgpr_read_b32 %0, a0\n\t"                    \
+                 "v_accvgpr_read_b32 %1, a1\n\ts_set_gpr_idx_off"                                      \
+                 : "=&v"(lo), "=&v"(hi)                                                              \
+                 : "s"((uint32_t)(r)))
+#define REG_PAIR(r, lo, hi)                                                                          \
+    do {                                                                                             \
+        const uint32_t _pr = (r);                                                                    \
+        if constexpr (BIG) {                                                                         \
+            if (_pr + 1 < kRegs) REG_PAIR_V(_pr, lo, hi);                                            \
+            else if (_pr >= kRegs) REG_PAIR_A(_pr - kRegs, lo, hi);                                  \
+            else { lo = REG_OF_V(_pr); hi = REG_OF_A(0); }                                           \
+        } else {                                                                                     \
+            REG_PAIR_V(_pr, lo, hi);                                                                 \
+        }                                                                                            \
+    } while (0)
+
 // lane i <- big-endian dword d + i of the unit (d wave-uniform): registers
 // R = d / 64 and R + 1 merged at lane d % 64 hold the 64 dwords rotated by
-// d % 64; one ds_bpermute puts them in order
+// d % 64; one ds_bpermute puts them in order (it reads lane addr[7:2], so
+// the rotation needs no masking: tools/micro/lds_packed3.hip)
 #define DW_LANES(dd)                                                                                 \
     ({                                                                                               \
         const uint32_t _d = (dd);                                                                    \
         const uint32_t _R = _d >> 6, _l0 = _d & 63;                                                  \
         /* R + 1 = 128 (v130, 32 KiB units) holds no unit data: those lanes lie past the */          \
         /* unit end, where every caller ignores them (past-L compares are clamped) */              \
-        const uint32_t _r0 = REG_OF(_R), _r1 = REG_OF(_R + 1);                                       \
+        uint32_t _r0, _r1;                                                                           \
+        REG_PAIR(_R, _r0, _r1);                                                                      \
         const uint32_t _m = lane >= _l0 ? _r0 : _r1;                                                 \
-        (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((_l0 + lane) & 63) << 2), (int)_m);            \
+        (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_d + lane) << 2), (int)_m); /* addr[7:2] */   \
     })
 
 // DPP across the whole wave: wave_shl:1 (lane l <- l + 1) and wave_shr:1
@@ -507,6 +535,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 {
     constexpr int W = SNAPPY_K1R_WINDOW;
     constexpr uint32_t DMAX = SNAPPY_K1R_DMAX;
+    static_assert(SNAPPY_K1R_LSMIN >= 4 && SNAPPY_K1R_LSMIN <= 32, "lane-space rounds need skip < 64 - 3");
     static_assert(DMAX >= 2 && DMAX <= 16, "DMAX: 2..16 (kcap <= 15 keeps the lane masks in range)");
     // 12 KiB: 4096 packed 3-byte records (u16 position, u8 tag) at byte 3 * slot:
     // one unaligned ds_read_b32 fetches position | tag << 16 (bits 24..31 are
@@ -598,8 +627,13 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     __syncthreads();
 
     uint2 *tok = tokens + (uint64_t)u * tok_cap;
-    uint32_t tka = 0, tkb = 0;  // 64 pending tokens, lane t holds token t
-    uint32_t nt = 0;
+    uint32_t tka = 0, tkb = 0;  // pending tokens: lane t < pend holds token nt + t
+    uint32_t nt = 0, pend = 0;
+    auto flush_tokens = [&]() {
+        if (lane < pend) tok[nt + lane] = make_uint2(tka, tkb);
+        nt += pend;
+        pend = 0;
+    };
 
     // ---- position window at q0 (see the header): dv = dwords q0/4 .. q0/4 + 63,
     // rotated: dword q0/4 + i sits at lane (dr + i) % 64 (ds_bpermute wraps addr[7:2])
@@ -614,10 +648,11 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         d0 = q0 >> 2;                                                                              \
         dr = d0 & 63;                                                                              \
         {                                                                                          \
-            const uint32_t _r0 = REG_OF(d0 >> 6), _r1 = REG_OF((d0 >> 6) + 1);                     \
+            uint32_t _r0, _r1;                                                                     \
+            REG_PAIR(d0 >> 6, _r0, _r1);                                                           \
             dv = lane >= dr ? _r0 : _r1;                                                           \
         }                                                                                          \
-        const uint32_t _k = dr + (((q0 & 3) + lane) >> 2);                                         \
+        const uint32_t _k = d0 + (((q0 & 3) + lane) >> 2); /* rotated by dr = d0 % 64 */         \
         const uint32_t _a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_k << 2), (int)dv);       \
         const uint32_t _b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_k + 1) << 2), (int)dv); \
         bv = funnel_bytes(_a, _b, perm_sel((q0 + lane) & 3));                                     \
@@ -630,7 +665,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         const uint32_t _pd = _bits ? (uint32_t)__builtin_ctz(_bits) : 0u;                          \
         pdl1 = _bits ? lane - _pd + 1 : 0xFFFFFF00u; /* signed: below every lane0 */             \
         pdc = q0 + lane - _pd;                                                                     \
-        const uint32_t _hp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - _pd) & 63) << 2), (int)hv); \
+        const uint32_t _hp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - _pd) << 2), (int)hv); \
         m_pdt = __ballot(_hp == hv);                                                               \
         /* probe lanes: <= 62 and not past is_block_end (L - p >= 16, 17 at skip 64) */           \
         const int32_t _w16 = (int32_t)(L - 16 - q0), _w17 = (int32_t)(L - 17 - q0);              \
@@ -665,8 +700,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         return len;
     };
     auto match_len = [&](uint32_t pf, uint32_t cand) -> uint32_t {
-        const uint32_t kp = (pf >> 2) - d0 + dr;
-        const uint32_t pa = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((kp + lane) << 2), (int)dv);
+        const uint32_t pa = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((pf >> 2) + lane) << 2), (int)dv);
         const uint32_t ca = DW_LANES(cand >> 2);
         const uint32_t pv = funnel_bytes(pa, wave_shl1(pa), perm_sel(pf & 3));
         const uint32_t cv = funnel_bytes(ca, wave_shl1(ca), perm_sel(cand & 3));
@@ -679,11 +713,23 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         return match_len_from(pf, cand, 64);
     };
     // emit_copy :323-329 as a token (the caller inserts pf into the table)
+    // (pend < 64 on entry: lane-space windows flush at refresh when more than
+    // 48 are pending -- a window of <= 62 probe positions holds <= 16 matches --
+    // and W-probe rounds flush when 64 are pending)
     auto put_token = [&](uint32_t pf, uint32_t len, uint32_t off) {
-        tka = (uint32_t)amdgcn_writelane((int)(pf | (len << 16)), (int)(nt & 63), (int)tka);
-        tkb = (uint32_t)amdgcn_writelane((int)off, (int)(nt & 63), (int)tkb);
-        nt++;
-        if ((nt & 63) == 0) tok[nt - 64 + lane] = make_uint2(tka, tkb);
+        tka = (uint32_t)amdgcn_writelane((int)(pf | (len << 16)), (int)pend, (int)tka);
+        tkb = (uint32_t)amdgcn_writelane((int)off, (int)pend, (int)tkb);
+        pend++;
+    };
+    // lane-space rounds defer a match's token into the next round, where its
+    // writelanes fill the wait for the verification gather (dka/dkb, dkn = 0/1;
+    // with dkn = 0 the writelanes hit lane pend, which the next token overwrites)
+    uint32_t dka = 0, dkb = 0, dkn = 0;
+    auto drain_token = [&]() {
+        tka = (uint32_t)amdgcn_writelane((int)dka, (int)pend, (int)tka);
+        tkb = (uint32_t)amdgcn_writelane((int)dkb, (int)pend, (int)tkb);
+        pend += dkn;
+        dkn = 0;
     };
 
 #ifdef SNAPPY_K1R_STATS
@@ -705,6 +751,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 LSTAMP(s0);
                 uint32_t lane0 = p - q0;
                 if (!lsw || lane0 + SNAPPY_K1R_RMIN > 62) {
+                    drain_token();
+                    if (pend > 48) flush_tokens();
                     WINDOW_LS(p - 1);
                     lane0 = 1;
                 }
@@ -735,7 +783,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     // find_copy_length :61-72 after found_match :259-265: lanes 0..15
                     // compare the 64 bytes at pf (dwords from dv) and c (registers)
                     const uint32_t pa = (uint32_t)__builtin_amdgcn_ds_bpermute(
-                        (int)(((pf >> 2) - d0 + dr + lane) << 2), (int)dv);
+                        (int)(((pf >> 2) + lane) << 2), (int)dv);
                     const uint32_t ca = DW_LANES(c >> 2);
                     __builtin_amdgcn_sched_barrier(0);
                     // the inserts known before the verdict: misses p_k - 1, p_k and the
@@ -743,19 +791,30 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     // first probe (its p - 1 is inserted only if it misses); other lanes
                     // write the dummy record
                     const uint32_t lo0 = f > lane0 ? lane0 - 1 : lane0;
+                    drain_token();
+#ifndef SNAPPY_K1R_EXP_NOINS
                     TBL_WRITE3(lane - lo0 <= f - lo0 ? adr : kDummy, word);
+#endif
                     LDS_ORDER();
+#ifndef SNAPPY_K1R_EXP_NOENT
                     ent = TBL_READ3(adr);
+#endif
                     LSTAMP(s2);
                     LSEG(1, s1, s2);
                     const uint32_t pv = funnel_bytes(pa, wave_shl1(pa), perm_sel(pf & 3));
                     const uint32_t cv = funnel_bytes(ca, wave_shl1(ca), perm_sel(c & 3));
                     const uint32_t y = pv ^ cv;
                     const uint64_t bad = __ballot(y != 0) & 0xFFFFull;
+                    // per lane: the prefix length if its dword holds the first mismatch
+                    const uint32_t lenv = 4 * lane + ((uint32_t)__builtin_clz(y | 1) >> 3);
                     uint32_t len;
+#ifdef SNAPPY_K1R_EXP_NOGATHER
+                    if (true) {
+                        len = 4 + ((c ^ pf) & 7);
+                    } else
+#endif
                     if (bad) {
-                        const uint32_t m = (uint32_t)__builtin_ctzll(bad);
-                        len = 4 * m + ((uint32_t)__builtin_clz(__builtin_amdgcn_readlane(y, m)) >> 3);
+                        len = __builtin_amdgcn_readlane(lenv, (uint32_t)__builtin_ctzll(bad));
                     } else {
                         len = match_len_from(pf, c, 64);
                     }
@@ -769,7 +828,11 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #ifdef SNAPPY_K1R_STATS
                         n_match++;
 #endif
-                        put_token(pf, len, pf - c);
+#ifndef SNAPPY_K1R_EXP_NOTOK
+                        dka = pf | (len << 16);
+                        dkb = pf - c;
+                        dkn = 1;
+#endif
                         np = pf + len;
                         skip = 32;
                     } else {  // tag collision: a miss (append_literal :283-287 steps by skip >> 5)
@@ -783,6 +846,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     }
                 } else {
                     const uint32_t nk = (uint32_t)__builtin_popcountll(valid);  // lanes lane0 .. lane0 + nk - 1
+                    drain_token();
                     // update_hash_table :303-307: p_k - 1 and p_k of every miss, lane order
                     TBL_WRITE3(lane - (lane0 - 1) <= nk ? adr : kDummy, word);
                     LDS_ORDER();
@@ -800,7 +864,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #ifdef SNAPPY_K1R_STATS
                 n_round++;
 #endif
-            } while (skip <= 64 - SNAPPY_K1R_LSMIN && !(L - p < (skip >> 5) + 15));
+            } while (skip <= 64 - SNAPPY_K1R_LSMIN && p <= L - 16);  // is_block_end at skip < 64
+            drain_token();
 #ifdef SNAPPY_K1R_STATS
             n_round--;
 #endif
@@ -849,6 +914,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #ifdef SNAPPY_K1R_STATS
                 n_match++;
 #endif
+                if (pend == 64) flush_tokens();
                 put_token(pf, len, pf - cand);
                 TBL_WRITE(hf & 0xFFFF, pf | (hf & 0xFFFF0000u));  // emit_copy :328
                 LDS_ORDER();
@@ -877,7 +943,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #undef TBL_WRITE3
 #undef TAG_EQ
 #undef LDS_ORDER
-    if (lane < (nt & 63)) tok[(nt & ~63u) + lane] = make_uint2(tka, tkb);
+    flush_tokens();
     if (lane == 0) ntok_out[u] = nt;
 #ifdef SNAPPY_K1R_STATS
     if (lane == 0) {

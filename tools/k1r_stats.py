@@ -3,7 +3,7 @@
 import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "lightweight-snappy_amd"))
-os.environ["SNAPPY_AMD_LIB"] = os.path.join(ROOT, "lightweight-snappy_amd", "variants", "libsnappy_amd_stats.so")
+os.environ["SNAPPY_AMD_LIB"] = os.path.join(ROOT, "lightweight-snappy_amd", "variants", "libsnappy_amd_" + os.environ.get("K1R_VARIANT", "stats") + ".so")
 import numpy as np, torch
 import datagen, snappy_amd
 kind = sys.argv[1] if len(sys.argv) > 1 else "T"

@@ -734,11 +734,11 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 
 #ifdef SNAPPY_K1R_STATS
     const uint64_t t_loop = clock64();
-    uint32_t n_probe = 0, n_match = 0, n_round = 0;
+    uint32_t n_probe = 0, n_match = 0, n_round = 0, n_refresh = 0;
 #endif
 #if defined(SNAPPY_K1R_LSTAMPS)
     uint64_t seg[6] = {0, 0, 0, 0, 0, 0};
-    uint64_t s0, s1, s2, s3, s4, s5;
+    uint64_t s0, s1, s2, s3, s4, s5, s6;
 #endif
     uint32_t p = 1, skip = 33;
     while (!(L - p < (skip >> 5) + 15)) {  // is_block_end :229-232
@@ -746,21 +746,32 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         n_round++;
 #endif
         if (skip <= 64 - SNAPPY_K1R_LSMIN) {
-            // ---------------- lane-space rounds until a step > 1 or the block end
-            do {
+            // ---------------- lane-space rounds until a step > 1 or the block end.
+            // The common round (a hit, verified, no refresh) is one straight-line
+            // path: the rare cases branch out of it (__builtin_expect).
+            auto refresh = [&]() {
+                LSTAMP(s5);
+#ifdef SNAPPY_K1R_STATS
+                n_refresh++;
+#endif
+                drain_token();
+                if (pend > 48) flush_tokens();
+                WINDOW_LS(p - 1);
+                LSTAMP(s6);
+                LSEG(5, s5, s6);
+            };
+            uint32_t lane0 = p - q0;
+            if (!lsw || lane0 + SNAPPY_K1R_RMIN > 62) {
+                refresh();
+                lane0 = 1;
+            }
+            for (;;) {
                 LSTAMP(s0);
-                uint32_t lane0 = p - q0;
-                if (!lsw || lane0 + SNAPPY_K1R_RMIN > 62) {
-                    drain_token();
-                    if (pend > 48) flush_tokens();
-                    WINDOW_LS(p - 1);
-                    lane0 = 1;
-                }
                 // probe k = lane - lane0 for k <= kcap: step 1 before it ((skip + k - 1) >> 5 == 1),
                 // predecessors within DMAX; inside the window and before is_block_end (m_win);
-                // the probe at skip + k == 64 needs L - p_k >= 17
+                // the probe at skip + k == 64 (only when 64 - skip < DMAX) needs L - p_k >= 17
                 uint64_t valid;
-                if (skip <= 64 - DMAX) {
+                if (__builtin_expect(skip <= 64 - DMAX, 1)) {  // skip is known before lane0
                     valid = (((1ull << DMAX) - 1) << lane0) & m_win;
                 } else {
                     const uint32_t kcap = 64 - skip;
@@ -776,7 +787,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 LSTAMP(s1);
                 LSEG(0, s0, s1);
                 uint32_t np;
-                if (hm) {
+                if (__builtin_expect(hm != 0, 1)) {
                     const uint32_t f = (uint32_t)__builtin_ctzll(hm);
                     const uint32_t pf = q0 + f;
                     const uint32_t c = __builtin_amdgcn_readlane(candv, f) & 0xFFFF;
@@ -792,13 +803,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     // write the dummy record
                     const uint32_t lo0 = f > lane0 ? lane0 - 1 : lane0;
                     drain_token();
-#ifndef SNAPPY_K1R_EXP_NOINS
                     TBL_WRITE3(lane - lo0 <= f - lo0 ? adr : kDummy, word);
-#endif
                     LDS_ORDER();
-#ifndef SNAPPY_K1R_EXP_NOENT
                     ent = TBL_READ3(adr);
-#endif
                     LSTAMP(s2);
                     LSEG(1, s1, s2);
                     const uint32_t pv = funnel_bytes(pa, wave_shl1(pa), perm_sel(pf & 3));
@@ -808,12 +815,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     // per lane: the prefix length if its dword holds the first mismatch
                     const uint32_t lenv = 4 * lane + ((uint32_t)__builtin_clz(y | 1) >> 3);
                     uint32_t len;
-#ifdef SNAPPY_K1R_EXP_NOGATHER
-                    if (true) {
-                        len = 4 + ((c ^ pf) & 7);
-                    } else
-#endif
-                    if (bad) {
+                    if (__builtin_expect(bad != 0, 1)) {
                         len = __builtin_amdgcn_readlane(lenv, (uint32_t)__builtin_ctzll(bad));
                     } else {
                         len = match_len_from(pf, c, 64);
@@ -823,16 +825,14 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #ifdef SNAPPY_K1R_STATS
                     n_probe += f - lane0 + 1;
 #endif
-                    if (len >= 4) {
-                        if (len > L - pf) len = L - pf;  // the compare never runs past the block
+                    if (__builtin_expect(len >= 4, 1)) {
+                        len = __builtin_elementwise_min(len, L - pf);  // the compare never runs past the block
 #ifdef SNAPPY_K1R_STATS
                         n_match++;
 #endif
-#ifndef SNAPPY_K1R_EXP_NOTOK
                         dka = pf | (len << 16);
                         dkb = pf - c;
                         dkn = 1;
-#endif
                         np = pf + len;
                         skip = 32;
                     } else {  // tag collision: a miss (append_literal :283-287 steps by skip >> 5)
@@ -845,6 +845,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                         skip += f - lane0 + 1;
                     }
                 } else {
+                    LSTAMP(s3);
                     const uint32_t nk = (uint32_t)__builtin_popcountll(valid);  // lanes lane0 .. lane0 + nk - 1
                     drain_token();
                     // update_hash_table :303-307: p_k - 1 and p_k of every miss, lane order
@@ -864,7 +865,14 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #ifdef SNAPPY_K1R_STATS
                 n_round++;
 #endif
-            } while (skip <= 64 - SNAPPY_K1R_LSMIN && p <= L - 16);  // is_block_end at skip < 64
+                // is_block_end at skip < 64; steps > 1 continue in W-probe rounds
+                if (__builtin_expect(!(skip <= 64 - SNAPPY_K1R_LSMIN && p <= L - 16), 0)) break;
+                lane0 = p - q0;
+                if (__builtin_expect(lane0 + SNAPPY_K1R_RMIN > 62, 0)) {
+                    refresh();
+                    lane0 = 1;
+                }
+            }
             drain_token();
 #ifdef SNAPPY_K1R_STATS
             n_round--;
@@ -952,11 +960,11 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #if defined(SNAPPY_K1R_LSTAMPS)
         st[1] = seg[0] | (seg[1] << 32);
         st[3] = seg[2] | (seg[3] << 32);
-        st[2] = seg[4];
+        st[2] = seg[4] | (seg[5] << 32);
 #else
         st[1] = 0;
         st[2] = n_probe | ((uint64_t)n_round << 32);
-        st[3] = n_match;
+        st[3] = n_match | ((uint64_t)n_refresh << 32);
 #endif
     }
 #endif

@@ -27,10 +27,10 @@ st = buf.reshape(units, 4)
 loop = st[:, 0].astype(float)
 seg0, seg1 = (st[:, 1] & 0xFFFFFFFF).astype(float), (st[:, 1] >> 32).astype(float)
 seg2, seg3 = (st[:, 3] & 0xFFFFFFFF).astype(float), (st[:, 3] >> 32).astype(float)
-seg4 = st[:, 2].astype(float)
+seg4, seg5 = (st[:, 2] & 0xFFFFFFFF).astype(float), (st[:, 2] >> 32).astype(float)
 rounds = int(os.environ.get("K1R_ROUNDS", "3937"))
-names = sys.argv[2].split(",") if len(sys.argv) > 2 else ["window", "lanes+bpermute", "table+conflict+ballot", "inserts+ballot2", "match/advance"]
+names = sys.argv[2].split(",") if len(sys.argv) > 2 and sys.argv[2] else ["head", "verify_issue", "verify_wait", "tail", "lane-space total", "window refresh"]
 tot = loop.sum()
-for nm, v in zip(names, [seg0, seg1, seg2, seg3, seg4]):
+for nm, v in zip(names, [seg0, seg1, seg2, seg3, seg4, seg5]):
     print(f"{nm:24s} {v.sum()/tot*100:5.1f}%  {v.mean()/rounds:7.1f} cycles/round")
 print(f"loop cycles/unit {loop.mean():.0f} ({loop.mean()/rounds:.0f}/round)")

@@ -28,8 +28,8 @@ hip = ctypes.CDLL("libamdhip64.so")
 buf = np.empty(units * 4, dtype=np.uint64)
 rc = hip.hipMemcpy(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ctx.tokens + units * tok_cap * 8), ctypes.c_size_t(buf.nbytes), 2)
 st = buf.reshape(units, 4)
-loop, tmatch, pr, matches = st[:, 0], st[:, 1], st[:, 2], st[:, 3]
+loop, tmatch, pr, matches, refresh = st[:, 0], st[:, 1], st[:, 2], st[:, 3] & 0xFFFFFFFF, st[:, 3] >> 32
 probes, rounds = pr & 0xFFFFFFFF, pr >> 32
-print(f"{kind}: units {units} probes/unit {probes.mean():.0f} rounds/unit {rounds.mean():.0f} matches/unit {matches.mean():.0f}")
+print(f"{kind}: units {units} probes/unit {probes.mean():.0f} rounds/unit {rounds.mean():.0f} matches/unit {matches.mean():.0f} window refreshes/unit {refresh.mean():.0f}")
 print(f"loop cycles/unit {loop.mean():.0f} cycles/probe {loop.sum() / probes.sum():.1f} cycles/round {loop.sum()/rounds.sum():.1f}"
       f" match-path cycles/match {tmatch.sum()/max(matches.sum(),1):.1f} non-match cycles/round {(loop.sum()-tmatch.sum())/rounds.sum():.1f}")

@@ -640,7 +640,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     uint32_t q0 = 0, d0 = 0, dr = 0, dv = 0, bv = 0, hv = 0;
     uint32_t pdl1 = 0, pdc = 0, ent = 0;      // lane-space data: predecessor lane + 1, its position, entry
     uint32_t adr = 0, word = 0;               // the lane's table record address and its insert word
-    uint64_t m_pdt = 0, m_win = 0, m_win17 = 0;
+    uint32_t pdnz = 0;
+    uint64_t m_win = 0, m_win17 = 0;
     bool lsw = false;  // the lane-space data describe the current window
 #define WINDOW_AT(qq)                                                                              \
     do {                                                                                           \
@@ -663,10 +664,11 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         WINDOW_AT(qq);                                                                             \
         const uint32_t _bits = same_x_bits<DMAX>((hv & 0xFFFF) + 1);                               \
         const uint32_t _pd = _bits ? (uint32_t)__builtin_ctz(_bits) : 0u;                          \
-        pdl1 = _bits ? lane - _pd + 1 : 0xFFFFFF00u; /* signed: below every lane0 */             \
+        /* lane - pd + 1, or lane - 1 at pd = 1: pdl1 >= lane0 also implies lane > lane0 */      \
+        pdl1 = _bits ? lane - _pd + 1 - (_pd == 1 ? 1u : 0u) : 0xFFFFFF00u; /* signed: below every lane0 */ \
         pdc = q0 + lane - _pd;                                                                     \
         const uint32_t _hp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - _pd) << 2), (int)hv); \
-        m_pdt = __ballot(_hp == hv);                                                               \
+        pdnz = _hp == hv ? 0u : 1u; /* 0 iff the predecessor's tag matches */                     \
         /* probe lanes: <= 62 and not past is_block_end (L - p >= 16, 17 at skip 64) */           \
         const int32_t _w16 = (int32_t)(L - 16 - q0), _w17 = (int32_t)(L - 17 - q0);              \
         m_win = __ballot((int32_t)lane <= _w16 && lane <= 62);                                     \
@@ -779,16 +781,17 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     if (lane0 + kcap < 64) valid &= ~((1ull << (lane0 + kcap)) & ~m_win17);
                     valid &= m_win;
                 }
-                // lane l > lane0 takes the in-round candidate when its nearest same-hash lane is >= lane0 - 1
-                const uint64_t m_inr = __ballot((int32_t)pdl1 >= (int32_t)lane0) & (~1ull << lane0);
-                const uint64_t m_tag = __ballot(TAG_EQ(ent, word));
-                const uint64_t hm = (m_tag ^ ((m_tag ^ m_pdt) & m_inr)) & valid;
-                const uint32_t candv = __builtin_amdgcn_inverse_ballot_w64(m_inr) ? pdc : ent;
+                // lane l > lane0 takes the in-round candidate when its nearest same-hash lane is >= lane0 - 1;
+                // the hit test selects per lane (VALU) so one ballot carries it to SALU
+                const bool inr = (int32_t)pdl1 >= (int32_t)lane0;
+                const uint32_t hitnz = inr ? pdnz : ((ent ^ word) & 0xFF0000u);
+                const uint64_t hm = __ballot(hitnz == 0) & valid;
+                const uint32_t candv = inr ? pdc : ent;
+                const uint32_t f = (uint32_t)__builtin_ctzll(hm);
                 LSTAMP(s1);
                 LSEG(0, s0, s1);
                 uint32_t np;
                 if (__builtin_expect(hm != 0, 1)) {
-                    const uint32_t f = (uint32_t)__builtin_ctzll(hm);
                     const uint32_t pf = q0 + f;
                     const uint32_t c = __builtin_amdgcn_readlane(candv, f) & 0xFFFF;
                     // find_copy_length :61-72 after found_match :259-265: lanes 0..15
@@ -814,12 +817,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     const uint64_t bad = __ballot(y != 0) & 0xFFFFull;
                     // per lane: the prefix length if its dword holds the first mismatch
                     const uint32_t lenv = 4 * lane + ((uint32_t)__builtin_clz(y | 1) >> 3);
-                    uint32_t len;
-                    if (__builtin_expect(bad != 0, 1)) {
-                        len = __builtin_amdgcn_readlane(lenv, (uint32_t)__builtin_ctzll(bad));
-                    } else {
-                        len = match_len_from(pf, c, 64);
-                    }
+                    // read before the test: with bad == 0 the lane index is garbage and len is replaced
+                    uint32_t len = __builtin_amdgcn_readlane(lenv, (uint32_t)__builtin_ctzll(bad) & 63);
+                    if (__builtin_expect(bad == 0, 0)) len = match_len_from(pf, c, 64);
                     LSTAMP(s3);
                     LSEG(2, s2, s3);
 #ifdef SNAPPY_K1R_STATS

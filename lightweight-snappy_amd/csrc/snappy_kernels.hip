@@ -675,8 +675,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         m_win17 = __ballot((int32_t)lane <= _w17 && lane <= 62);                                   \
         adr = 3 * (hv & 0xFFFF);                                                                   \
         word = (q0 + lane) | (hv & 0xFF0000u);                                                     \
-        ent = TBL_READ3(adr);                                                                      \
-        lsw = true;                                                                                \
+        lsw = true; /* the caller reads ent */                                                     \
     } while (0)
 
     // find_copy_length :61-72 after found_match :259-265: common prefix of the
@@ -767,6 +766,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 refresh();
                 lane0 = 1;
             }
+            // the round's table entries: read once per round, at its end, after every
+            // insert of the round (one definition, so no register copy waits for it)
+            ent = TBL_READ3(adr);
             for (;;) {
                 LSTAMP(s0);
                 // probe k = lane - lane0 for k <= kcap: step 1 before it ((skip + k - 1) >> 5 == 1),
@@ -808,7 +810,6 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     drain_token();
                     TBL_WRITE3(lane - lo0 <= f - lo0 ? adr : kDummy, word);
                     LDS_ORDER();
-                    ent = TBL_READ3(adr);
                     LSTAMP(s2);
                     LSEG(1, s1, s2);
                     const uint32_t pv = funnel_bytes(pa, wave_shl1(pa), perm_sel(pf & 3));
@@ -839,7 +840,6 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                         if (f == lane0) {  // its p - 1, then p again (the later write wins)
                             TBL_WRITE3(lane - (lane0 - 1) <= 1 ? adr : kDummy, word);
                             LDS_ORDER();
-                            ent = TBL_READ3(adr);
                         }
                         np = pf + ((skip + f - lane0) >> 5);
                         skip += f - lane0 + 1;
@@ -851,7 +851,6 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     // update_hash_table :303-307: p_k - 1 and p_k of every miss, lane order
                     TBL_WRITE3(lane - (lane0 - 1) <= nk ? adr : kDummy, word);
                     LDS_ORDER();
-                    ent = TBL_READ3(adr);
                     np = q0 + lane0 + nk - 1 + ((skip + nk - 1) >> 5);  // the last probe steps by 2 at skip 64
                     skip += nk;
 #ifdef SNAPPY_K1R_STATS
@@ -872,6 +871,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     refresh();
                     lane0 = 1;
                 }
+                ent = TBL_READ3(adr);
             }
             drain_token();
 #ifdef SNAPPY_K1R_STATS

@@ -755,8 +755,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #ifdef SNAPPY_K1R_STATS
                 n_refresh++;
 #endif
-                drain_token();
-                if (pend > 48) flush_tokens();
+                // the deferred token stays pending (drained by the next round): count it
+                if (pend + dkn > 48) flush_tokens();
                 WINDOW_LS(p - 1);
                 LSTAMP(s6);
                 LSEG(5, s5, s6);
@@ -771,6 +771,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             ent = TBL_READ3(adr);
             for (;;) {
                 LSTAMP(s0);
+                drain_token();  // the previous round's match: one writelane pair per round
                 // probe k = lane - lane0 for k <= kcap: step 1 before it ((skip + k - 1) >> 5 == 1),
                 // predecessors within DMAX; inside the window and before is_block_end (m_win);
                 // the probe at skip + k == 64 (only when 64 - skip < DMAX) needs L - p_k >= 17
@@ -807,7 +808,6 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     // first probe (its p - 1 is inserted only if it misses); other lanes
                     // write the dummy record
                     const uint32_t lo0 = f > lane0 ? lane0 - 1 : lane0;
-                    drain_token();
                     TBL_WRITE3(lane - lo0 <= f - lo0 ? adr : kDummy, word);
                     LDS_ORDER();
                     LSTAMP(s2);
@@ -847,7 +847,6 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 } else {
                     LSTAMP(s3);
                     const uint32_t nk = (uint32_t)__builtin_popcountll(valid);  // lanes lane0 .. lane0 + nk - 1
-                    drain_token();
                     // update_hash_table :303-307: p_k - 1 and p_k of every miss, lane order
                     TBL_WRITE3(lane - (lane0 - 1) <= nk ? adr : kDummy, word);
                     LDS_ORDER();

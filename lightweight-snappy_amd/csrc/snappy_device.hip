@@ -27,6 +27,8 @@ struct snappy_amd_ctx {
     size_t tokens_cap = 0;
     uint32_t *ntok = nullptr;
     size_t ntok_cap = 0;
+    uint32_t *seg_off = nullptr;    // K2 segment offsets inside each unit
+    size_t seg_off_cap = 0;
     int32_t *status = nullptr;
     size_t status_cap = 0;
     uint64_t *total = nullptr;      // device u64
@@ -113,7 +115,7 @@ void snappy_amd_destroy(snappy_amd_ctx *c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void *bufs[] = {c->scratch, c->sizes, c->tokens, c->ntok, c->status, c->total, c->k5res, c->d_a, c->d_b, c->d_idx,
+    void *bufs[] = {c->scratch, c->sizes, c->tokens, c->ntok, c->seg_off, c->status, c->total, c->k5res, c->d_a, c->d_b, c->d_idx,
                     c->k5buf};
     for (void *b : bufs) if (b) (void)hipFree(b);
     if (c->h_total) (void)hipHostFree(c->h_total);
@@ -203,6 +205,10 @@ static int compress_impl(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t
             return rc;
         if ((rc = grow(reinterpret_cast<void **>(&c->ntok), &c->ntok_cap, units * sizeof(uint32_t)))) return rc;
         if ((rc = grow(reinterpret_cast<void **>(&c->sizes), &c->sizes_cap, units * sizeof(uint32_t)))) return rc;
+        // segments per unit: tokens 0..ntok (the tail literal is token ntok <= tok_cap - 1)
+        const uint32_t segs = (tok_cap + SNAPPY_K2_SEG - 1) / SNAPPY_K2_SEG;
+        if ((rc = grow(reinterpret_cast<void **>(&c->seg_off), &c->seg_off_cap, units * segs * sizeof(uint32_t))))
+            return rc;
         const uint32_t hm = hdr_mode_of(layout, flags);
         if (c->timing) (void)hipEventRecord(c->ev[0], c->stream);
         // units <= 32 KiB: unit in VGPRs (3 waves/SIMD); 64 KiB blocks: VGPRs + AGPRs (1 wave/SIMD)
@@ -212,19 +218,19 @@ static int compress_impl(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t
         if (unit <= SNAPPY_K1R_MAX_UNIT)
             hipLaunchKernelGGL(k1r_match_units, dim3((uint32_t)units), dim3(64), dyn_lds, c->stream,
                                static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens,
-                               tok_cap, c->ntok, c->sizes);
+                               tok_cap, c->ntok, c->sizes, c->seg_off, segs);
         else
             hipLaunchKernelGGL(k1r_match_units64, dim3((uint32_t)units), dim3(64), 0, c->stream,
                                static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens,
-                               tok_cap, c->ntok, c->sizes);
+                               tok_cap, c->ntok, c->sizes, c->seg_off, segs);
         HIP_OK(hipGetLastError());
         if (c->timing) (void)hipEventRecord(c->ev[1], c->stream);
-        hipLaunchKernelGGL(k2s_size_units, dim3((uint32_t)units), dim3(64), 0, c->stream, (uint64_t)n, unit, hm,
-                           header_value, c->tokens, tok_cap, c->ntok, c->sizes);
         hipLaunchKernelGGL(k3_scan, dim3(1), dim3(1024), 0, c->stream, c->sizes, (uint64_t)units, d_offsets, c->total);
-        hipLaunchKernelGGL(k2_emit_units, dim3((uint32_t)units), dim3(64), 0, c->stream,
+        // K1r wrote the sizes and segment offsets; K2: a few waves per unit, each taking
+        // every SNAPPY_K2_WAVES-th segment (text fills ~12 segments of 32 KiB units)
+        hipLaunchKernelGGL(k2_emit_units, dim3((uint32_t)units, segs < SNAPPY_K2_WAVES ? segs : SNAPPY_K2_WAVES), dim3(64), 0, c->stream,
                            static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens, tok_cap,
-                           c->ntok, d_offsets, static_cast<uint8_t *>(d_out));
+                           c->ntok, c->seg_off, segs, d_offsets, static_cast<uint8_t *>(d_out));
         HIP_OK(hipGetLastError());
         if (c->timing) (void)hipEventRecord(c->ev[2], c->stream);
         goto done;

@@ -36,17 +36,19 @@ __global__ void k1_compress_units(const uint8_t *__restrict__ in, uint64_t n, ui
                                   uint64_t stride, uint32_t *__restrict__ sizes);
 __global__ void k1r_match_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit, uint32_t hdr_mode,
                                 uint64_t header_value, uint2 *__restrict__ tokens, uint32_t tok_cap,
-                                uint32_t *__restrict__ ntok_out, uint32_t *__restrict__ sizes);
+                                uint32_t *__restrict__ ntok_out, uint32_t *__restrict__ sizes,
+                                uint32_t *__restrict__ seg_off, uint32_t segs);
 __global__ void k1r_match_units64(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit, uint32_t hdr_mode,
                                 uint64_t header_value, uint2 *__restrict__ tokens, uint32_t tok_cap,
-                                uint32_t *__restrict__ ntok_out, uint32_t *__restrict__ sizes);
-__global__ void k2s_size_units(uint64_t n, uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
-                               const uint2 *__restrict__ tokens, uint32_t tok_cap, const uint32_t *__restrict__ ntok,
-                               uint32_t *__restrict__ sizes);
+                                uint32_t *__restrict__ ntok_out, uint32_t *__restrict__ sizes,
+                                uint32_t *__restrict__ seg_off, uint32_t segs);
 __global__ void k2_emit_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit, uint32_t hdr_mode,
                               uint64_t header_value, const uint2 *__restrict__ tokens, uint32_t tok_cap,
-                              const uint32_t *__restrict__ ntok, const uint64_t *__restrict__ offsets,
-                              uint8_t *__restrict__ out);
+                              const uint32_t *__restrict__ ntok, const uint32_t *__restrict__ seg_off, uint32_t segs,
+                              const uint64_t *__restrict__ offsets, uint8_t *__restrict__ out);
+// K2 segments: 256 tokens (4 per lane); waves per unit
+#define SNAPPY_K2_SEG 256u
+#define SNAPPY_K2_WAVES 8u
 // register-resident K1r handles units up to this size (128 VGPRs x 64 lanes x 4 B)
 #define SNAPPY_K1R_MAX_UNIT 32768u
 

@@ -528,10 +528,43 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
 #define LSEG(i, a, b) do { } while (0)
 #endif
 
+// K2 segments: 4 consecutive tokens per lane, 256 per wave
+constexpr uint32_t kK2Per = 4;
+constexpr uint32_t kK2Seg = 64 * kK2Per;
+
+// Wave-wide inclusive add-scan in DPP (row_shr 1/2/4/8 inside 16-lane rows,
+// then row_bcast:15 / row_bcast:31 across rows): no LDS round trips.
+template <uint32_t CTRL, uint32_t ROWS>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, true);
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
+{
+    x += dpp0<0x111, 0xF>(x);
+    x += dpp0<0x112, 0xF>(x);
+    x += dpp0<0x114, 0xF>(x);
+    x += dpp0<0x118, 0xF>(x);
+    x += dpp0<0x142, 0xA>(x);
+    x += dpp0<0x143, 0xC>(x);
+    return x;
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, uint32_t *total)
+{
+    (void)lane;
+    const uint32_t x = wave_incl_scan(v);
+    *total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+    return x - v;
+}
+
 template <bool BIG>
 __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
+                                         uint32_t hdr_mode, uint64_t header_value,
                                          uint2 *__restrict__ tokens, uint32_t tok_cap,
-                                         uint32_t *__restrict__ ntok_out)
+                                         uint32_t *__restrict__ ntok_out, uint32_t *__restrict__ sizes,
+                                         uint32_t *__restrict__ seg_off, uint32_t segs)
 {
     constexpr int W = SNAPPY_K1R_WINDOW;
     constexpr uint32_t DMAX = SNAPPY_K1R_DMAX;
@@ -629,8 +662,25 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     uint2 *tok = tokens + (uint64_t)u * tok_cap;
     uint32_t tka = 0, tkb = 0;  // pending tokens: lane t < pend holds token nt + t
     uint32_t nt = 0, pend = 0;
+    // encoded size so far (header, literals, copies: src/snappy_compression.c:95-165)
+    // and the end of the last flushed token; K2 segments start every kK2Seg tokens
+    uint32_t acc = 0, cend = 0;
+    if (hdr_mode == SNAPPY_HDR_EVERY_UNIT) acc = varint_len(L);
+    else if (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0) acc = varint_len(header_value);
+    uint32_t *const segu = seg_off + (uint64_t)u * segs;
     auto flush_tokens = [&]() {
-        if (lane < pend) tok[nt + lane] = make_uint2(tka, tkb);
+        const bool has = lane < pend;
+        if (has) tok[nt + lane] = make_uint2(tka, tkb);
+        const uint32_t pos = tka & 0xFFFF, len = tka >> 16, end = pos + len;
+        // lane l <- end of lane l - 1; lane 0 keeps cend (no bound_ctrl: the old value stays)
+        const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp((int)cend, (int)end, 0x138, 0xF, 0xF, false);
+        const uint32_t litn = pos - prev;
+        const uint32_t b = has ? (litn ? literal_bytes(litn) : 0u) + copy_bytes(len, tkb) : 0u;
+        uint32_t tot;
+        const uint32_t ex = wave_excl_scan(b, lane, &tot);
+        if (has && ((nt + lane) & (kK2Seg - 1)) == 0) segu[(nt + lane) / kK2Seg] = acc + ex;
+        if (pend) cend = __builtin_amdgcn_readlane(end, pend - 1);
+        acc += tot;
         nt += pend;
         pend = 0;
     };
@@ -951,7 +1001,12 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #undef TAG_EQ
 #undef LDS_ORDER
     flush_tokens();
-    if (lane == 0) ntok_out[u] = nt;
+    // the tail literal is pseudo-token nt (src/snappy_compression.c:292-297)
+    if (lane == 0) {
+        if ((nt & (kK2Seg - 1)) == 0) segu[nt / kK2Seg] = acc;
+        ntok_out[u] = nt;
+        sizes[u] = acc + (L > cend ? literal_bytes(L - cend) : 0u);
+    }
 #ifdef SNAPPY_K1R_STATS
     if (lane == 0) {
         uint64_t *st = reinterpret_cast<uint64_t *>(tokens + (uint64_t)gridDim.x * tok_cap) + 4 * (uint64_t)u;
@@ -973,12 +1028,10 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
                                                           uint32_t hdr_mode, uint64_t header_value,
                                                           uint2 *__restrict__ tokens, uint32_t tok_cap,
                                                           uint32_t *__restrict__ ntok_out,
-                                                          uint32_t *__restrict__ sizes)
+                                                          uint32_t *__restrict__ sizes,
+                                                          uint32_t *__restrict__ seg_off, uint32_t segs)
 {
-    (void)hdr_mode;
-    (void)header_value;
-    (void)sizes;
-    k1r_body<false>(in, n, unit, tokens, tok_cap, ntok_out);
+    k1r_body<false>(in, n, unit, hdr_mode, header_value, tokens, tok_cap, ntok_out, sizes, seg_off, segs);
 }
 
 // 65,536-byte blocks (the reference's MAX_BLOCK_SIZE): unit in 128 VGPRs +
@@ -987,12 +1040,10 @@ __global__ __launch_bounds__(64, 1) void k1r_match_units64(const uint8_t *__rest
                                                             uint32_t hdr_mode, uint64_t header_value,
                                                             uint2 *__restrict__ tokens, uint32_t tok_cap,
                                                             uint32_t *__restrict__ ntok_out,
-                                                            uint32_t *__restrict__ sizes)
+                                                            uint32_t *__restrict__ sizes,
+                                                            uint32_t *__restrict__ seg_off, uint32_t segs)
 {
-    (void)hdr_mode;
-    (void)header_value;
-    (void)sizes;
-    k1r_body<true>(in, n, unit, tokens, tok_cap, ntok_out);
+    k1r_body<true>(in, n, unit, hdr_mode, header_value, tokens, tok_cap, ntok_out, sizes, seg_off, segs);
 }
 
 // ---------------------------------------------------------------------------
@@ -1002,33 +1053,6 @@ __global__ __launch_bounds__(64, 1) void k1r_match_units64(const uint8_t *__rest
 // them out (src/snappy_compression.c:95-165).  The last pseudo-token carries
 // the tail literal.
 // ---------------------------------------------------------------------------
-// Wave-wide inclusive add-scan in DPP (row_shr 1/2/4/8 inside 16-lane rows,
-// then row_bcast:15 / row_bcast:31 across rows): no LDS round trips.
-template <uint32_t CTRL, uint32_t ROWS>
-__device__ __forceinline__ uint32_t dpp0(uint32_t x)
-{
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, true);
-}
-
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
-{
-    x += dpp0<0x111, 0xF>(x);
-    x += dpp0<0x112, 0xF>(x);
-    x += dpp0<0x114, 0xF>(x);
-    x += dpp0<0x118, 0xF>(x);
-    x += dpp0<0x142, 0xA>(x);
-    x += dpp0<0x143, 0xC>(x);
-    return x;
-}
-
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, uint32_t *total)
-{
-    (void)lane;
-    const uint32_t x = wave_incl_scan(v);
-    *total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-    return x - v;
-}
-
 // exclusive add-scan over lanes 0..31 only (lanes 32..63 undefined), total of lanes 0..31
 __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v, uint32_t *total)
 {
@@ -1054,50 +1078,8 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t x)
     return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
-// K2s: exact encoded size of every unit from its token list (header +
-// literal headers/bytes + copy pieces), one wave per unit, one token per lane.
-__global__ __launch_bounds__(64) void k2s_size_units(uint64_t n, uint32_t unit, uint32_t hdr_mode,
-                                                     uint64_t header_value, const uint2 *__restrict__ tokens,
-                                                     uint32_t tok_cap, const uint32_t *__restrict__ ntok,
-                                                     uint32_t *__restrict__ sizes)
-{
-    const uint32_t lane = threadIdx.x;
-    const uint32_t u = blockIdx.x;
-    const uint64_t base = (uint64_t)u * unit;
-    const uint32_t L = (uint32_t)((n - base) < unit ? (n - base) : unit);
-    uint32_t enc = 0;
-    if (hdr_mode == SNAPPY_HDR_EVERY_UNIT) enc = varint_len(L);
-    else if (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0) enc = varint_len(header_value);
-    const uint2 *tok = tokens + (uint64_t)u * tok_cap;
-    const uint32_t nt = ntok[u];
-    uint32_t carry = 0, acc = 0;
-    for (uint32_t c = 0; c <= nt; c += 64) {
-        const uint32_t t = c + lane;
-        uint32_t pos = L, len = 0, off = 0;
-        if (t < nt) {
-            const uint2 k = tok[t];
-            pos = k.x & 0xFFFF;
-            len = k.x >> 16;
-            off = k.y;
-        }
-        const uint32_t end = pos + len;
-        uint32_t prev_end = (uint32_t)__shfl_up((int)end, 1, 64);
-        if (lane == 0) prev_end = carry;
-        uint32_t b = 0;
-        if (t <= nt) {
-            const uint32_t litn = pos - prev_end;
-            b = (litn ? literal_bytes(litn) : 0) + (len ? copy_bytes(len, off) : 0);
-        }
-        acc += b;
-        carry = (uint32_t)__shfl((int)end, 63, 64);
-    }
-    // wave sum
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) acc += (uint32_t)__shfl_xor((int)acc, d, 64);
-    if (lane == 0) sizes[u] = enc + acc;
-}
-
-__device__ __forceinline__ void put_copy(uint8_t *o, uint32_t len, uint32_t off)
+template <typename P>
+__device__ __forceinline__ void put_copy(P *o, uint32_t len, uint32_t off)
 {
     while (len > 68) {
         o[0] = 0xFE; o[1] = (uint8_t)off; o[2] = (uint8_t)(off >> 8);
@@ -1115,66 +1097,211 @@ __device__ __forceinline__ void put_copy(uint8_t *o, uint32_t len, uint32_t off)
     }
 }
 
+// the element bytes of one token (literal header + payload + copy pieces) at w;
+// literal bytes come from src + s0 (global); litn <= 16 by five independent dword
+// loads realigned with v_alignbyte, longer literals are left to the caller
+template <typename P>
+__device__ __forceinline__ void put_element(P *w, const uint8_t *__restrict__ src, uint32_t s0, uint32_t litn,
+                                            uint32_t hl, uint32_t len, uint32_t off, bool wide_ok)
+{
+    if (hl == 1) w[0] = (uint8_t)((litn - 1) << 2);
+    else if (hl == 2) { w[0] = 60 << 2; w[1] = (uint8_t)(litn - 1); }
+    else if (hl == 3) { w[0] = 61 << 2; w[1] = (uint8_t)(litn - 1); w[2] = (uint8_t)((litn - 1) >> 8); }
+    if (litn <= 16) {
+        if (wide_ok) {
+            const uintptr_t sa = reinterpret_cast<uintptr_t>(src + s0);
+            const uint32_t sh = (uint32_t)(sa & 3);
+            const uint32_t *aw = reinterpret_cast<const uint32_t *>(sa - sh);
+            const uint32_t d0 = aw[0], d1 = aw[1], d2 = aw[2], d3 = aw[3], d4 = aw[4];
+            const uint32_t r[4] = {__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                                   __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh)};
+#pragma unroll
+            for (uint32_t j = 0; j < 16; j++)
+                if (j < litn) w[hl + j] = (uint8_t)(r[j >> 2] >> (8 * (j & 3)));
+        } else {
+            for (uint32_t j = 0; j < litn; j++) w[hl + j] = src[s0 + j];
+        }
+    }
+    if (len) put_copy(w + hl + litn, len, off);
+}
+
+// K2: tokens -> bytes at the unit's final offset (write_literal :95-120,
+// write_copy :153-165).  One wave per (unit, segment of kK2Seg tokens, 4
+// consecutive per lane): each wave makes a single pass with two memory round
+// trips (tokens, then literal bytes), so the latency of one unit's passes is
+// spread over many waves.  The pass is assembled in LDS (byte writes are cheap
+// there) and leaves as aligned dword stores; larger passes (long copies /
+// literals) write HBM directly.
+constexpr uint32_t kK2Stage = 8192;
+
+// the whole wave copies literal k (long: > 16 bytes) of every lane/slot in
+// longs into the LDS stage; 8 byte loads per lane in flight per round trip
+__device__ __forceinline__ void k2_long_literals(__attribute__((address_space(3))) uint8_t *w,
+                                                 const uint8_t *__restrict__ src, uint64_t longs, uint32_t litn,
+                                                 uint32_t s0v, uint32_t d0v, uint32_t lane)
+{
+    while (longs) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(longs);
+        longs &= longs - 1;
+        const uint32_t ln = __builtin_amdgcn_readlane(litn, k);
+        const uint32_t s0 = __builtin_amdgcn_readlane(s0v, k);
+        const uint32_t d0 = __builtin_amdgcn_readlane(d0v, k);
+        for (uint32_t j0 = 0; j0 < ln; j0 += 512) {
+            uint8_t v[8];
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++) {
+                const uint32_t j = j0 + 64 * q + lane;
+                v[q] = j < ln ? src[s0 + j] : 0;
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++) {
+                const uint32_t j = j0 + 64 * q + lane;
+                if (j < ln) w[d0 + j] = v[q];
+            }
+        }
+    }
+}
+
+// the same straight to HBM: byte head up to an aligned destination dword, then
+// aligned dword stores of source dwords realigned by v_alignbyte (8 loads per
+// lane in flight, 1 KiB per round trip), byte tail; end = in + n bounds reads
+__device__ __forceinline__ void k2_long_literals(uint8_t *w, const uint8_t *__restrict__ src,
+                                                 const uint8_t *__restrict__ end, uint64_t longs, uint32_t litn,
+                                                 uint32_t s0v, uint32_t d0v, uint32_t lane)
+{
+    while (longs) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(longs);
+        longs &= longs - 1;
+        const uint32_t ln = __builtin_amdgcn_readlane(litn, k);
+        const uint8_t *s = src + __builtin_amdgcn_readlane(s0v, k);
+        uint8_t *d = w + __builtin_amdgcn_readlane(d0v, k);
+        uint32_t head = (uint32_t)((4 - (reinterpret_cast<uintptr_t>(d) & 3)) & 3);
+        if (head > ln) head = ln;
+        if (lane < head) d[lane] = s[lane];
+        const uint32_t nw = (ln - head) >> 2;
+        const uint8_t *sb = s + head;
+        const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(sb) & 3);
+        const uint32_t *sa = reinterpret_cast<const uint32_t *>(sb - sh);
+        uint32_t *dw = reinterpret_cast<uint32_t *>(d + head);
+        for (uint32_t k0 = 0; k0 < nw; k0 += 256) {
+            uint32_t lo[4], hi[4];
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++) {
+                const uint32_t kk = k0 + 64 * q + lane;
+                lo[q] = hi[q] = 0;
+                if (kk < nw) {
+                    lo[q] = sa[kk];
+                    if (sh) {
+                        const uint8_t *pb = reinterpret_cast<const uint8_t *>(sa + kk + 1);
+                        if (pb + 4 <= end) hi[q] = sa[kk + 1];
+                        else for (uint32_t t = 0; t < sh; t++) hi[q] |= (uint32_t)pb[t] << (8 * t);
+                    }
+                }
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++) {
+                const uint32_t kk = k0 + 64 * q + lane;
+                if (kk < nw) dw[kk] = __builtin_amdgcn_alignbyte(hi[q], lo[q], sh);
+            }
+        }
+        const uint32_t t0 = head + 4 * nw;
+        if (lane < ln - t0) d[t0 + lane] = s[t0 + lane];
+    }
+}
+
 __global__ __launch_bounds__(64) void k2_emit_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
                                                     uint32_t hdr_mode, uint64_t header_value,
                                                     const uint2 *__restrict__ tokens, uint32_t tok_cap,
                                                     const uint32_t *__restrict__ ntok,
+                                                    const uint32_t *__restrict__ seg_off, uint32_t segs,
                                                     const uint64_t *__restrict__ offsets, uint8_t *__restrict__ out)
 {
+    __shared__ __attribute__((aligned(16))) uint8_t stage_[kK2Stage + 16];
+    auto *const stage = (__attribute__((address_space(3))) uint8_t *)stage_;
     const uint32_t lane = threadIdx.x;
     const uint32_t u = blockIdx.x;
+    const uint32_t nt = ntok[u];
     const uint64_t base = (uint64_t)u * unit;
     const uint32_t L = (uint32_t)((n - base) < unit ? (n - base) : unit);
     const uint8_t *src = in + base;
     uint8_t *dst = out + offsets[u];
-    uint32_t o = 0;
-    if (hdr_mode == SNAPPY_HDR_EVERY_UNIT) o = varint_put(L, dst, lane);
-    else if (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0) o = varint_put(header_value, dst, lane);
-
     const uint2 *tok = tokens + (uint64_t)u * tok_cap;
-    const uint32_t nt = ntok[u];
-    uint32_t carry = 0;  // end of the previous token = start of this literal
-    for (uint32_t c = 0; c <= nt; c += 64) {
-        const uint32_t t = c + lane;
-        uint32_t pos = L, len = 0, off = 0;  // pseudo-token: tail literal
-        bool live = t <= nt;
+    if (blockIdx.y == 0) {
+        if (hdr_mode == SNAPPY_HDR_EVERY_UNIT) varint_put(L, dst, lane);
+        else if (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0) varint_put(header_value, dst, lane);
+    }
+    for (uint32_t sg = blockIdx.y; sg * kK2Seg <= nt; sg += gridDim.y) {
+    const uint32_t c = sg * kK2Seg;
+    const uint32_t o = seg_off[(uint64_t)u * segs + sg];
+    // end of the previous segment's last token = start of this segment's first literal
+    uint32_t carry = 0;
+    if (c) {
+        const uint2 k = tok[c - 1];
+        carry = (k.x & 0xFFFF) + (k.x >> 16);
+    }
+
+    uint32_t pos[kK2Per], len[kK2Per], off[kK2Per], pe[kK2Per], litn[kK2Per], hl[kK2Per], sz[kK2Per];
+    bool live[kK2Per];
+#pragma unroll
+    for (uint32_t i = 0; i < kK2Per; i++) {
+        const uint32_t t = c + kK2Per * lane + i;
+        pos[i] = L; len[i] = 0; off[i] = 0;  // pseudo-token: tail literal
+        live[i] = t <= nt;
         if (t < nt) {
             const uint2 k = tok[t];
-            pos = k.x & 0xFFFF;
-            len = k.x >> 16;
-            off = k.y;
-            if (len == 0) len = 65536;  // unreachable for units <= 32 KiB
+            pos[i] = k.x & 0xFFFF;
+            len[i] = k.x >> 16;
+            off[i] = k.y;
+            if (len[i] == 0) len[i] = 65536;  // unreachable for units <= 32 KiB
         }
-        const uint32_t end = pos + len;
-        uint32_t prev_end = (uint32_t)__shfl_up((int)end, 1, 64);
-        if (lane == 0) prev_end = carry;
-        const uint32_t litn = live ? pos - prev_end : 0;
-        const uint32_t hl = litn ? (litn <= 60 ? 1 : (litn <= 256 ? 2 : 3)) : 0;
-        const uint32_t cb = (live && len) ? copy_bytes(len, off) : 0;
-        uint32_t total;
-        const uint32_t my = o + wave_excl_scan(hl + litn + cb, lane, &total);
-        if (live) {
-            uint8_t *w = dst + my;
-            if (hl == 1) w[0] = (uint8_t)((litn - 1) << 2);
-            else if (hl == 2) { w[0] = 60 << 2; w[1] = (uint8_t)(litn - 1); }
-            else if (hl == 3) { w[0] = 61 << 2; w[1] = (uint8_t)(litn - 1); w[2] = (uint8_t)((litn - 1) >> 8); }
-            if (litn <= 16) {
-                for (uint32_t j = 0; j < litn; j++) w[hl + j] = src[prev_end + j];
-            }
-            if (len) put_copy(w + hl + litn, len, off);
+    }
+    uint32_t pe0 = (uint32_t)__shfl_up((int)(pos[kK2Per - 1] + len[kK2Per - 1]), 1, 64);
+    if (lane == 0) pe0 = carry;
+    uint32_t lsum = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kK2Per; i++) {
+        pe[i] = i ? pos[i - 1] + len[i - 1] : pe0;
+        litn[i] = live[i] ? pos[i] - pe[i] : 0;
+        hl[i] = litn[i] ? (litn[i] <= 60 ? 1 : (litn[i] <= 256 ? 2 : 3)) : 0;
+        sz[i] = hl[i] + litn[i] + ((live[i] && len[i]) ? copy_bytes(len[i], off[i]) : 0);
+        lsum += sz[i];
+    }
+    uint32_t total;
+    uint32_t rel = wave_excl_scan(lsum, lane, &total);
+    const bool staged = total <= kK2Stage;
+    uint64_t longs[kK2Per];
+    uint32_t d0v[kK2Per];
+#pragma unroll
+    for (uint32_t i = 0; i < kK2Per; i++) {
+        const bool wide_ok = base + pe[i] + 20 <= n;  // the aligned 20-byte read ends inside in[0, n)
+        if (live[i]) {
+            if (staged) put_element(stage + rel, src, pe[i], litn[i], hl[i], len[i], off[i], wide_ok);
+            else put_element(dst + o + rel, src, pe[i], litn[i], hl[i], len[i], off[i], wide_ok);
         }
-        // long literals: the whole wave copies each one
-        uint64_t longs = __ballot(live && litn > 16);
-        while (longs) {
-            const uint32_t k = (uint32_t)__builtin_ctzll(longs);
-            longs &= longs - 1;
-            const uint32_t ln = __builtin_amdgcn_readlane(litn, k);
-            const uint32_t s0 = __builtin_amdgcn_readlane(prev_end, k);
-            const uint32_t d0 = __builtin_amdgcn_readlane(my + hl, k);
-            for (uint32_t j = lane; j < ln; j += 64) dst[d0 + j] = src[s0 + j];
-        }
-        carry = (uint32_t)__shfl((int)end, 63, 64);
-        o += total;
+        longs[i] = __ballot(live[i] && litn[i] > 16);
+        d0v[i] = rel + hl[i];
+        rel += sz[i];
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kK2Per; i++) {
+        if (staged) k2_long_literals(stage, src, longs[i], litn[i], pe[i], d0v[i], lane);
+        else k2_long_literals(dst + o, src, in + n, longs[i], litn[i], pe[i], d0v[i], lane);
+    }
+    if (staged) {
+        __builtin_amdgcn_wave_barrier();
+        // stage[0, total) -> dst + o: byte head to a dword boundary, dwords, byte tail
+        uint8_t *g = dst + o;
+        uint32_t head = (uint32_t)((4 - (reinterpret_cast<uintptr_t>(g) & 3)) & 3);
+        if (head > total) head = total;
+        if (lane < head) g[lane] = stage[lane];
+        const uint32_t nw = (total - head) >> 2;
+        uint32_t *gw = reinterpret_cast<uint32_t *>(g + head);
+        for (uint32_t k = lane; k < nw; k += 64)
+            gw[k] = *(const __attribute__((address_space(3))) u32u *)(stage + head + 4 * k);
+        const uint32_t tail0 = head + 4 * nw;
+        if (lane < total - tail0) g[tail0 + lane] = stage[tail0 + lane];
+    }
+    __builtin_amdgcn_wave_barrier();  // the stage is reused by the next segment
     }
 }
 

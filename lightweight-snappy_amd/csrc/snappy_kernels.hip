@@ -1134,6 +1134,56 @@ __device__ __forceinline__ void put_element(P *w, const uint8_t *__restrict__ sr
 // literals) write HBM directly.
 constexpr uint32_t kK2Stage = 8192;
 
+// put_element into the LDS stage without exec-mask branches: every store is
+// issued by every lane, lanes without a byte to store hit their own dummy
+// slot (stage + kK2Stage + 4 lane); full literal dwords as unaligned ds_write_b32
+__device__ __forceinline__ void put_element_lds(__attribute__((address_space(3))) uint8_t *stage, uint32_t at,
+                                                const uint8_t *__restrict__ src, uint32_t s0, uint32_t litn,
+                                                uint32_t hl, uint32_t len, uint32_t off, bool wide_ok, bool live,
+                                                uint32_t lane)
+{
+    const uint32_t dum = kK2Stage + 4 * lane;
+#define K2_ST8(cond, adr, v) stage[(cond) ? (adr) : dum] = (uint8_t)(v)
+    // literal header (write_literal :95-120)
+    const uint32_t lm1 = litn - 1;
+    K2_ST8(live && hl >= 1, at, hl == 1 ? lm1 << 2 : (hl == 2 ? 60u << 2 : 61u << 2));
+    K2_ST8(live && hl >= 2, at + 1, lm1);
+    K2_ST8(live && hl == 3, at + 2, lm1 >> 8);
+    const uint32_t lp = at + hl;
+    if (litn <= 16) {
+        if (wide_ok) {
+            const uintptr_t sa = reinterpret_cast<uintptr_t>(src + s0);
+            const uint32_t sh = (uint32_t)(sa & 3);
+            const uint32_t *aw = reinterpret_cast<const uint32_t *>(sa - sh);
+            const uint32_t d0 = aw[0], d1 = aw[1], d2 = aw[2], d3 = aw[3], d4 = aw[4];
+            const uint32_t r0 = __builtin_amdgcn_alignbyte(d1, d0, sh), r1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+            const uint32_t r2 = __builtin_amdgcn_alignbyte(d3, d2, sh), r3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+#define K2_ST32(k, r) *(__attribute__((address_space(3))) u32u *)(stage + (live && 4 * (k) + 4 <= litn ? lp + 4 * (k) : dum)) = (r)
+            K2_ST32(0, r0); K2_ST32(1, r1); K2_ST32(2, r2); K2_ST32(3, r3);
+#undef K2_ST32
+            const uint32_t fb = litn & ~3u, rem = litn & 3u;
+            const uint32_t rt = fb == 0 ? r0 : (fb == 4 ? r1 : (fb == 8 ? r2 : r3));
+            K2_ST8(live && rem > 0, lp + fb, rt);
+            K2_ST8(live && rem > 1, lp + fb + 1, rt >> 8);
+            K2_ST8(live && rem > 2, lp + fb + 2, rt >> 16);
+        } else if (live) {
+            for (uint32_t j = 0; j < litn; j++) stage[lp + j] = src[s0 + j];
+        }
+    }
+    // copy (write_copy :153-165): one piece when len <= 64, the split otherwise
+    const uint32_t cp = lp + litn;
+    if (len <= 64) {
+        const bool c1 = len < 12 && off < 2048;
+        const bool has = live && len != 0;
+        K2_ST8(has, cp, c1 ? (((off >> 8) << 5) + ((len - 4) << 2) + 1) : (((len - 1) << 2) | 2));
+        K2_ST8(has, cp + 1, off);
+        K2_ST8(has && !c1, cp + 2, off >> 8);
+    } else if (live) {
+        put_copy(stage + cp, len, off);
+    }
+#undef K2_ST8
+}
+
 // the whole wave copies literal k (long: > 16 bytes) of every lane/slot in
 // longs into the LDS stage; 8 byte loads per lane in flight per round trip
 __device__ __forceinline__ void k2_long_literals(__attribute__((address_space(3))) uint8_t *w,
@@ -1216,7 +1266,7 @@ __global__ __launch_bounds__(64) void k2_emit_units(const uint8_t *__restrict__ 
                                                     const uint32_t *__restrict__ seg_off, uint32_t segs,
                                                     const uint64_t *__restrict__ offsets, uint8_t *__restrict__ out)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t stage_[kK2Stage + 16];
+    __shared__ __attribute__((aligned(16))) uint8_t stage_[kK2Stage + 4 * 64 + 16];  // + per-lane dummy slots
     auto *const stage = (__attribute__((address_space(3))) uint8_t *)stage_;
     const uint32_t lane = threadIdx.x;
     const uint32_t u = blockIdx.x;
@@ -1274,10 +1324,8 @@ __global__ __launch_bounds__(64) void k2_emit_units(const uint8_t *__restrict__ 
 #pragma unroll
     for (uint32_t i = 0; i < kK2Per; i++) {
         const bool wide_ok = base + pe[i] + 20 <= n;  // the aligned 20-byte read ends inside in[0, n)
-        if (live[i]) {
-            if (staged) put_element(stage + rel, src, pe[i], litn[i], hl[i], len[i], off[i], wide_ok);
-            else put_element(dst + o + rel, src, pe[i], litn[i], hl[i], len[i], off[i], wide_ok);
-        }
+        if (staged) put_element_lds(stage, rel, src, pe[i], litn[i], hl[i], len[i], off[i], wide_ok, live[i], lane);
+        else if (live[i]) put_element(dst + o + rel, src, pe[i], litn[i], hl[i], len[i], off[i], wide_ok);
         longs[i] = __ballot(live[i] && litn[i] > 16);
         d0v[i] = rel + hl[i];
         rel += sz[i];

@@ -333,7 +333,6 @@ typedef uint16_t __attribute__((aligned(1))) u16u;
 
 constexpr uint32_t kTagMul = 0x9E3779B1u;
 constexpr uint32_t kRegs = 128;  // VGPRs holding a 32 KiB unit (64 dwords each), + 1 zero spare
-
 // Register r (wave-uniform) of the resident unit.  g0..g3 are pinned to
 // v2..v129 by the asm constraints (65,536-byte units continue in a0..a128),
 // so the relative move (s_set_gpr_idx_on, SRC0) is exact whatever else the
@@ -1132,7 +1131,11 @@ __device__ __forceinline__ void put_element(P *w, const uint8_t *__restrict__ sr
 // spread over many waves.  The pass is assembled in LDS (byte writes are cheap
 // there) and leaves as aligned dword stores; larger passes (long copies /
 // literals) write HBM directly.
-constexpr uint32_t kK2Stage = 8192;
+// 4 KiB holds a text segment (~2 KiB of output) and keeps K2 at 32 waves per CU
+#ifndef SNAPPY_K2_STAGE
+#define SNAPPY_K2_STAGE 4096
+#endif
+constexpr uint32_t kK2Stage = SNAPPY_K2_STAGE;
 
 // put_element into the LDS stage without exec-mask branches: every store is
 // issued by every lane, lanes without a byte to store hit their own dummy
@@ -1259,7 +1262,12 @@ __device__ __forceinline__ void k2_long_literals(uint8_t *w, const uint8_t *__re
     }
 }
 
-__global__ __launch_bounds__(64) void k2_emit_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
+// 1: no register cap (88 VGPRs, 5 waves/SIMD); 6 or 8 waves spill to scratch and
+// measured no better (tools/variant_bench.py, 256 MiB text: 0.295 / 0.294 / 0.325 ms)
+#ifndef SNAPPY_K2_WAVES_PER_EU
+#define SNAPPY_K2_WAVES_PER_EU 1
+#endif
+__global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
                                                     uint32_t hdr_mode, uint64_t header_value,
                                                     const uint2 *__restrict__ tokens, uint32_t tok_cap,
                                                     const uint32_t *__restrict__ ntok,
@@ -1356,27 +1364,58 @@ __global__ __launch_bounds__(64) void k2_emit_units(const uint8_t *__restrict__ 
 // ---------------------------------------------------------------------------
 // K3a: exclusive scan of unit sizes -> offsets[0..count], total.
 // ---------------------------------------------------------------------------
+// One workgroup walks the sizes in tiles of 8,192 staged through LDS
+// (coalesced loads and stores); each thread scans 8 consecutive sizes, DPP
+// scans combine threads within a wave and the 16 wave totals.  A unit is at
+// most ~67.6 KB, so a tile's relative prefix fits 32 bits; the carry is 64-bit.
+constexpr uint32_t kScanPer = 8;
+constexpr uint32_t kScanTile = 1024 * kScanPer;
+
 __global__ __launch_bounds__(1024) void k3_scan(const uint32_t *__restrict__ sizes, uint64_t count,
                                                 uint64_t *__restrict__ offsets, uint64_t *__restrict__ total)
 {
-    __shared__ uint64_t part[1024];
-    const uint32_t t = threadIdx.x;
-    const uint64_t per = (count + 1023) / 1024;
-    const uint64_t b0 = t * per < count ? t * per : count;
-    const uint64_t b1 = b0 + per < count ? b0 + per : count;
-    uint64_t s = 0;
-    for (uint64_t i = b0; i < b1; i++) s += sizes[i];
-    part[t] = s;
-    __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {
-        const uint64_t v = t >= d ? part[t - d] : 0;
+    __shared__ uint32_t tile[kScanTile + kScanTile / 32];  // + one pad dword per 32 (bank spread)
+    __shared__ uint32_t wtot[16];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+#define K3_AT(i) ((i) + ((i) >> 5))
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < count; b += kScanTile) {
+        const uint32_t m = (uint32_t)(count - b < kScanTile ? count - b : kScanTile);
+        for (uint32_t i = t; i < kScanTile; i += 1024) tile[K3_AT(i)] = i < m ? sizes[b + i] : 0u;
         __syncthreads();
-        part[t] += v;
+        uint32_t v[kScanPer], s = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kScanPer; k++) {
+            v[k] = tile[K3_AT(t * kScanPer + k)];
+            s += v[k];
+        }
+        const uint32_t x = wave_incl_scan(s);
+        if (lane == 63) wtot[w] = x;
+        __syncthreads();
+        if (w == 0) {
+            const uint32_t y = lane < 16 ? wtot[lane] : 0u;
+            const uint32_t z = wave_incl_scan(y);
+            if (lane < 16) wtot[lane] = z - y;  // exclusive over waves
+        }
+        __syncthreads();
+        uint32_t run = wtot[w] + x - s;
+#pragma unroll
+        for (uint32_t k = 0; k < kScanPer; k++) {
+            tile[K3_AT(t * kScanPer + k)] = run;
+            run += v[k];
+        }
+        __syncthreads();
+        for (uint32_t i = t; i < m; i += 1024) offsets[b + i] = carry + tile[K3_AT(i)];
+        if (t == 1023) wtot[0] = run;  // the tile's total
+        __syncthreads();
+        carry += wtot[0];
         __syncthreads();
     }
-    uint64_t run = t ? part[t - 1] : 0;
-    for (uint64_t i = b0; i < b1; i++) { offsets[i] = run; run += sizes[i]; }
-    if (t == 1023) { offsets[count] = part[1023]; *total = part[1023]; }
+#undef K3_AT
+    if (t == 0) {
+        offsets[count] = carry;
+        *total = carry;
+    }
 }
 
 // ---------------------------------------------------------------------------

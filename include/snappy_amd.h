@@ -36,6 +36,7 @@ extern "C" {
 #define SNAPPY_AMD_ERR_DEVICE (-7)     /* HIP runtime error / no device           */
 #define SNAPPY_AMD_ERR_IO (-8)         /* FILE* read/write failure                */
 #define SNAPPY_AMD_ERR_UNSUPPORTED (-9)
+#define SNAPPY_AMD_ERR_TIMEOUT (-10)   /* a block waited too long for an earlier one  */
 
 /* Block size of the reference stream format (src/snappy_compression.c:9). */
 #define SNAPPY_AMD_BLOCK 65536u
@@ -106,9 +107,20 @@ int snappy_amd_compress_device_ex(snappy_amd_ctx *ctx, const void *d_in, size_t 
                                   uint32_t flags, uint64_t header_value, void *d_out, uint64_t *d_offsets,
                                   size_t *out_len);
 
+/* Block index entries (d_offsets, nunits+1 u64): bits [0,40) = byte offset in
+ * the stream of the element holding the unit's first output byte; bits
+ * [40,64) = how many output bytes of that element precede the unit (0 when
+ * the element starts the unit -- always the case for streams this library
+ * writes, whose entries are therefore plain offsets).  The last entry is the
+ * stream's end.  Non-zero skips arise only in foreign SINGLE streams whose
+ * elements cross 65,536-byte output boundaries (snappy_amd_index_device). */
+#define SNAPPY_AMD_IDX_OFFSET_BITS 40
+
 /* Decode what compress_device produced (or any stream whose block index is
- * given): n = total decoded bytes, d_offsets = the unit index.  Returns the
- * first failing unit's status (synchronises to read it). */
+ * given): n = total decoded bytes, d_offsets = the unit index.  SINGLE
+ * layout decodes any valid stream: elements may straddle blocks and copies
+ * may reach into earlier blocks (those blocks run in a second, ordered pass).
+ * Returns the first failing unit's status (synchronises to read it). */
 int snappy_amd_decompress_device(snappy_amd_ctx *ctx, const void *d_comp, const uint64_t *d_offsets,
                                  size_t n, uint32_t chunk, int layout, void *d_out);
 
@@ -124,9 +136,10 @@ int snappy_amd_decompress_device_ex(snappy_amd_ctx *ctx, const void *d_comp, con
                                     int sync);
 
 /* Build the block index of a SINGLE-layout stream already in HBM (e.g. a
- * file produced by the reference): d_offsets gets ceil(N/65536)+1 entries,
- * *n_out the declared length N.  Fails with SNAPPY_AMD_ERR_UNSUPPORTED if an
- * element straddles a 65536-byte block boundary. */
+ * file produced by the reference or another encoder): d_offsets gets
+ * ceil(N/65536)+1 entries (format above), *n_out the declared length N.
+ * SNAPPY_AMD_ERR_UNSUPPORTED only if a straddling element starts past 2^40
+ * bytes or covers a boundary more than 2^24 - 1 bytes after its start. */
 int snappy_amd_index_device(snappy_amd_ctx *ctx, const void *d_comp, size_t clen, uint64_t *d_offsets,
                             size_t max_units, size_t *n_out);
 

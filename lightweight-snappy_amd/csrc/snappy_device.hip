@@ -106,6 +106,8 @@ int snappy_amd_create(int device, snappy_amd_ctx **out)
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k4_decompress_units),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k4_decompress_back),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     *out = c;
     return SNAPPY_AMD_OK;
 }
@@ -115,8 +117,8 @@ void snappy_amd_destroy(snappy_amd_ctx *c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void *bufs[] = {c->scratch, c->sizes, c->tokens, c->ntok, c->seg_off, c->status, c->total, c->k5res, c->d_a, c->d_b, c->d_idx,
-                    c->k5buf};
+    void *bufs[] = {c->scratch, c->sizes, c->tokens, c->ntok, c->seg_off, c->status, c->total, c->k5res,
+                    c->d_a, c->d_b, c->d_idx, c->k5buf};
     for (void *b : bufs) if (b) (void)hipFree(b);
     if (c->h_total) (void)hipHostFree(c->h_total);
     if (c->h_status) (void)hipHostFree(c->h_status);
@@ -291,18 +293,29 @@ static int decompress_launch(snappy_amd_ctx *c, const void *d_comp, const uint64
     c->last_units = 0;
     if (n == 0) return SNAPPY_AMD_OK;
     const size_t units = (n + unit - 1) / unit;
+    if (units > 0xFFFFFFFFull) return SNAPPY_AMD_ERR_ARG;
     int rc;
-    if ((rc = grow(reinterpret_cast<void **>(&c->status), &c->status_cap, units * sizeof(int32_t)))) return rc;
-    // a unit's compressed size is bounded by the encoder's worst case; the
-    // decoder rejects (TRUNCATED) anything larger than this LDS window.
-    const uint32_t comp_cap = (uint32_t)(((uint64_t)unit + unit / 32 + 64 + 15) & ~15ull);
+    // status: one word per unit + pass 2's ticket counter and defer flag
+    if ((rc = grow(reinterpret_cast<void **>(&c->status), &c->status_cap, (units + 2) * sizeof(int32_t)))) return rc;
+    // one whole stream (SINGLE): elements may straddle blocks and copies may
+    // reach into earlier blocks (src/snappy_decompression.c:253-280, 345-363);
+    // pass 1 decodes every self-contained block, pass 2 the others in order
+    const uint32_t allow_back = layout == SNAPPY_AMD_SINGLE ? 1u : 0u;
     if (c->timing) (void)hipEventRecord(c->ev[3], c->stream);
+    if (allow_back) HIP_OK(hipMemsetAsync(c->status + units, 0, 2 * sizeof(int32_t), c->stream));
     const uint32_t ring = k4_ring_bytes(unit);
-    hipLaunchKernelGGL(k4_decompress_units, dim3((uint32_t)units), dim3(64), ring, c->stream,
-                       static_cast<const uint8_t *>(d_comp), d_offsets, (uint64_t)n, unit, hdr_mode_of(layout, flags),
-                       header_value, comp_cap, ring,
-                       static_cast<uint8_t *>(d_out), c->status);
+    const uint32_t hm = hdr_mode_of(layout, flags);
+    // dynamic LDS: the ring + 16 bytes of per-unit scalars
+    hipLaunchKernelGGL(k4_decompress_units, dim3((uint32_t)units), dim3(64), ring + 16, c->stream,
+                       static_cast<const uint8_t *>(d_comp), d_offsets, (uint64_t)n, unit, hm, header_value, ring,
+                       allow_back, static_cast<uint8_t *>(d_out), c->status);
     HIP_OK(hipGetLastError());
+    if (allow_back) {
+        hipLaunchKernelGGL(k4_decompress_back, dim3((uint32_t)units), dim3(64), ring + 16, c->stream,
+                           static_cast<const uint8_t *>(d_comp), d_offsets, (uint64_t)n, unit, hm, header_value, ring,
+                           static_cast<uint8_t *>(d_out), c->status);
+        HIP_OK(hipGetLastError());
+    }
     if (c->timing) (void)hipEventRecord(c->ev[4], c->stream);
     c->last_units = units;
     return SNAPPY_AMD_OK;
@@ -324,8 +337,12 @@ int snappy_amd_decompress_status(snappy_amd_ctx *c)
     HIP_OK(hipMemcpyAsync(c->h_status, c->status, bytes, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
     if (c->timing) (void)hipEventElapsedTime(&c->k4_ms, c->ev[3], c->ev[4]);
-    for (size_t i = 0; i < c->last_units; i++)
+    for (size_t i = 0; i < c->last_units; i++) {
+        // DEFER survives only in a STREAMS unit (no pass 2): a copy reaching
+        // before the start of its own stream
+        if (c->h_status[i] > 0) return SNAPPY_AMD_ERR_OFFSET;
         if (c->h_status[i] != SNAPPY_ST_OK) return c->h_status[i];
+    }
     return SNAPPY_AMD_OK;
 }
 

@@ -21,6 +21,9 @@
 #define SNAPPY_ST_OVERRUN (-5)
 #define SNAPPY_ST_CAPACITY (-6)
 #define SNAPPY_ST_UNSUPPORTED (-9)
+#define SNAPPY_ST_TIMEOUT (-10)   // K4 pass 2: a unit waited too long for an earlier one
+#define SNAPPY_ST_DEFER 2         // K4 pass 1: the unit copies from earlier units (pass 2 decodes it;
+                                  // meanwhile its status is DEFER + output bytes already in HBM)
 
 namespace snappy_amd {
 
@@ -56,10 +59,18 @@ __global__ void k3_scan(const uint32_t *__restrict__ sizes, uint64_t count, uint
                         uint64_t *__restrict__ total);
 __global__ void k3_gather(const uint8_t *__restrict__ scratch, uint64_t stride, const uint32_t *__restrict__ sizes,
                           const uint64_t *__restrict__ offsets, uint8_t *__restrict__ out);
+// K4 pass 1: every unit; allow_back = 1 for SINGLE-layout streams (straddling
+// elements and copies into earlier blocks are legal: such units end with
+// status SNAPPY_ST_DEFER, for pass 2, and set status[units + 1])
 __global__ void k4_decompress_units(const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets,
                                     uint64_t n, uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
-                                    uint32_t comp_cap, uint32_t ring,
-                                    uint8_t *__restrict__ out, int32_t *__restrict__ status);
+                                    uint32_t ring, uint32_t allow_back, uint8_t *__restrict__ out,
+                                    int32_t *__restrict__ status);
+// K4 pass 2: the DEFER units, in ticket order (status[units] = ticket counter,
+// status[units + 1] = pass 1's defer flag; both 0 before pass 1)
+__global__ void k4_decompress_back(const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets,
+                                   uint64_t n, uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
+                                   uint32_t ring, uint8_t *__restrict__ out, int32_t *__restrict__ status);
 constexpr uint32_t K5_CHUNK = 16384;  // == K5_S in the kernels
 __global__ void k5a_chunk_walk(const uint8_t *__restrict__ comp, uint64_t clen, uint64_t *__restrict__ X,
                                uint64_t *__restrict__ O);

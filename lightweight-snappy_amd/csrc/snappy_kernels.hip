@@ -18,6 +18,7 @@
 // candidate, exactly as in the reference (snappy_compression.c:259-265).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #include "snappy_kernels.h"
 
@@ -1445,17 +1446,37 @@ __global__ __launch_bounds__(256) void k3_gather(const uint8_t *__restrict__ scr
 }
 
 // ---------------------------------------------------------------------------
-// K4: one wave per unit; LDS holds only the decoded window (unit bytes), so
-// 32 KiB units run 5 per CU.  The compressed unit streams through a 512-byte
+// K4: one wave per unit.  The compressed unit streams through a 512-byte
 // register window (cur = bytes [B, B+256), nxt = [B+256, B+512), one dword
-// per lane, nxt prefetched a window ahead); tags are parsed in SALU from
-// v_readlane, elements are executed lane-parallel into LDS: literals from the
-// window by ds_bpermute (long ones straight from HBM), copies as one LDS read
-// + write per <= 64 bytes with the byte-serial overlap semantics of
-// src/snappy_decompression.c:273-280 (out[op+j] = out[op-off + j mod off]).
-// Tag dispatch of :290-333 with bounds checks; a copy reaching before the
-// unit start is an error here (the reference compressor never emits one).
+// per lane, nxt prefetched a window ahead).  Each batch parses the elements
+// starting in the next 64 window bytes lane-parallel (tag dispatch of
+// src/snappy_decompression.c:290-333, element chain by pointer doubling),
+// then executes them in 64-byte output passes into an LDS ring that is
+// flushed to HBM in 1 KiB blocks; copies keep the byte-serial overlap
+// semantics of :273-280 (out[op+j] = out[op-off + j mod off]).
+//
+// Block index entries (include/snappy_amd.h): bits [0,40) = compressed
+// offset of the element holding the unit's first output byte, bits [40,64) =
+// how many of that element's output bytes precede the unit (0 when the
+// element starts the unit, always so for streams this codec writes).  A
+// unit whose first element straddles in resumes it; a unit whose last
+// element straddles out truncates it (the reference decodes one whole
+// output buffer, :345-363, so elements may cross 65,536-byte boundaries and
+// copies may reach into earlier blocks, :253-280).
+//
+// Pass 1 (k4_decompress_units, BACK = false) decodes every unit whose copies
+// stay inside it; a unit needing bytes of earlier units stops with status
+// DEFER.  Pass 2 (k4_decompress_back, BACK = true) runs only those: units
+// take tickets in index order (so every unit a wave waits for is already
+// resident or finished), publish their HBM progress with release stores and
+// wait with acquire loads until the bytes their copies read are in HBM.
 // ---------------------------------------------------------------------------
+constexpr uint64_t kIdxOffMask = (1ull << 40) - 1;
+constexpr uint32_t kIdxSkipShift = 40;
+constexpr int32_t kK4Tail = 3;  // pass 1, in-batch: an element runs past the unit's end
+// pass 2 keeps a deferred unit's progress in its status word: DEFER + bytes in
+// HBM while it runs, its final status (<= 0) once done
+
 __device__ __forceinline__ uint32_t load_dw_guarded(const uint8_t *comp, uint64_t a, uint64_t lim)
 {
     // dword at 4-aligned absolute address a; bytes at or past lim read as 0
@@ -1488,6 +1509,65 @@ __device__ __forceinline__ void k4_flush(const uint8_t *ob, uint32_t M, uint8_t 
     }
 }
 
+// literal bytes lsrc[0, kl) straight from HBM to output [kop, kop+kl), in
+// HBM and in the ring (later copies read its tail)
+__device__ __forceinline__ void k4_literal_hbm(const uint8_t *lsrc, uint32_t kl, uint32_t kop, uint8_t *ob, uint32_t M,
+                                               uint8_t *dst, uint32_t lane)
+{
+#pragma unroll 1
+    for (uint32_t b = 0; b < kl; b += 256) {
+        uint8_t v[4];
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            const uint32_t jj = b + 64 * m + lane;
+            v[m] = jj < kl ? lsrc[jj] : 0;
+        }
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            const uint32_t jj = b + 64 * m + lane;
+            if (jj < kl) {
+                ob[(kop + jj) & M] = v[m];
+                dst[kop + jj] = v[m];
+            }
+        }
+    }
+}
+
+// pass 2: this unit's output [0, F) is in HBM, or (val <= 0) it is done
+// (release: the wave's stores first, then the status word)
+__device__ __forceinline__ void k4_publish(int32_t *status, uint32_t u, int32_t val, uint32_t lane)
+{
+    if (lane == 0) __hip_atomic_store(status + u, val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// pass 2: wait until output bytes [g_lo, g_hi] (global positions below this
+// unit) are in HBM.  Units [done_lo, u) are known complete.  Every unit waited
+// for has a lower ticket than this one, so it is running or done; the time
+// limit only guards against a corrupt progress array.
+__device__ __noinline__ int32_t k4_wait(const int32_t *status, uint64_t g_lo, uint64_t g_hi, uint32_t unit,
+                                        uint32_t lane, uint32_t *done_lo)
+{
+    const uint32_t vlo = (uint32_t)(g_lo / unit), vhi = (uint32_t)(g_hi / unit);
+    for (uint32_t v = vhi + 1; v-- > vlo;) {
+        if (v >= *done_lo) continue;
+        const int32_t need = v == vhi ? (int32_t)(g_hi - (uint64_t)v * unit) + 1 : (int32_t)unit;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            int32_t p = 0;
+            if (lane == 0) p = __hip_atomic_load(status + v, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            p = __builtin_amdgcn_readfirstlane(p);
+            if (p <= 0) {  // done (pass 1 or 2; an error status lets the caller fail on its own)
+                if (v + 1 == *done_lo) *done_lo = v;
+                break;
+            }
+            if (p - SNAPPY_ST_DEFER >= need) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 30ull * 100000000ull) return SNAPPY_ST_TIMEOUT;  // 100 MHz clock
+            __builtin_amdgcn_s_sleep(4);
+        }
+    }
+    return SNAPPY_ST_OK;
+}
+
 #ifdef SNAPPY_K4_STATS
 __device__ uint64_t g_k4_stats[32768 * 8];
 #define K4STAMP(var)                                                                        \
@@ -1500,39 +1580,60 @@ __device__ uint64_t g_k4_stats[32768 * 8];
 #define K4STAMP(var) do { } while (0)
 #endif
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_decompress_units(const uint8_t *__restrict__ comp,
-                                                          const uint64_t *__restrict__ offsets, uint64_t n,
-                                                          uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
-                                                          uint32_t comp_cap, uint32_t ring, uint8_t *__restrict__ out,
-                                                          int32_t *__restrict__ status)
+template <bool BACK>
+__device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets,
+                                        uint64_t n, uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
+                                        uint32_t ring, uint32_t allow_back, uint8_t *__restrict__ out,
+                                        int32_t *__restrict__ status, uint32_t u)
 {
+    // copy source positions: relative to the unit start, negative = an earlier unit (pass 2 only)
+    using SrcT = typename std::conditional<BACK, int64_t, uint32_t>::type;
     extern __shared__ uint32_t lds[];
     uint8_t *ob = reinterpret_cast<uint8_t *>(lds);  // output ring: position x -> ob[x & M]
     const uint32_t M = ring - 1;
     const uint32_t lane = threadIdx.x;
-    const uint32_t u = blockIdx.x;
-    const uint64_t c0 = offsets[u], c1 = offsets[u + 1];
+    const uint64_t ix0 = offsets[u], ix1 = offsets[u + 1];
+    const uint64_t c0 = ix0 & kIdxOffMask, c1n = ix1 & kIdxOffMask;
+    const uint32_t skip0 = (uint32_t)(ix0 >> kIdxSkipShift), skip1 = (uint32_t)(ix1 >> kIdxSkipShift);
     const uint64_t base = (uint64_t)u * unit;
     const uint32_t want = (uint32_t)((n - base) < unit ? (n - base) : unit);
     int32_t st = SNAPPY_ST_OK;
-    if (c1 < c0 || c1 - c0 > comp_cap) {
-        if (lane == 0) status[u] = SNAPPY_ST_TRUNCATED;
-        return;
-    }
-    const uint32_t clen = (uint32_t)(c1 - c0);
+    // the unit's compressed bytes: up to the next entry, or (its last element
+    // straddling out) as far as the stream goes
+    uint64_t c1 = c1n;
+    if (skip1) c1 = offsets[(n + unit - 1) / unit] & kIdxOffMask;
+    if (c1 > c0 + 0x7FFFFFFFull) c1 = c0 + 0x7FFFFFFFull;
+    if (c1 < c0 || ((skip0 | skip1) && !allow_back)) st = SNAPPY_ST_TRUNCATED;
+    const uint32_t clen = st == SNAPPY_ST_OK ? (uint32_t)(c1 - c0) : 0u;
     uint8_t *dst = out + base;
     uint32_t F = 0;  // output bytes [0, F) are in HBM; [F, op) only in the ring
+    uint32_t done_lo = u;  // pass 2: units [done_lo, u) are complete
+    // pass 2 checks every element in VALU; pass 1 keeps its loop state small and
+    // resolves the rare cases (an element running past the unit, a copy into
+    // an earlier unit) in scalar code after the batch ballot
+    // the element the next unit resumes (skip1 > 0) starts here: it may run past the unit
+    const uint32_t tail_ip = skip1 && c1n >= c0 && c1n - c0 < clen ? (uint32_t)(c1n - c0) : 0xFFFFFFFFu;
+    // copies may reach this far before the unit start
+    const uint32_t back_lim = (uint32_t)(base < 0xFFFFFFFFull ? base : 0xFFFFFFFFull);
+    // pass 1 re-reads the tail element's position from LDS (past the ring) on its rare path
+    volatile uint32_t *tail_lds = lds + ring / 4;
+    if (!BACK && lane == 0) {
+        tail_lds[0] = tail_ip;
+        tail_lds[1] = want - skip1;
+    }
 
     // register window over the compressed unit (absolute 4-aligned base B)
     uint64_t B = c0 & ~3ull;
-    uint32_t cur = load_dw_guarded(comp, B + 4 * lane, c1);
-    uint32_t nxt = load_dw_guarded(comp, B + 256 + 4 * lane, c1);
+    uint32_t cur = load_dw_guarded(comp, B + 4 * lane, c0 + clen);
+    uint32_t nxt = load_dw_guarded(comp, B + 256 + 4 * lane, c0 + clen);
+    c1 = c0 + clen;
     // dword k (0..127) of [cur | nxt], k uniform
 #define WDW(k) ((uint32_t)((k) < 64 ? __builtin_amdgcn_readlane(cur, (k)) : __builtin_amdgcn_readlane(nxt, (k) - 64)))
 
     uint32_t ip = 0, op = 0;  // ip relative to c0
     // varint preamble: every STREAMS unit, and block 0 of a SINGLE stream
-    if (hdr_mode == SNAPPY_HDR_EVERY_UNIT || (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0)) {
+    if (st == SNAPPY_ST_OK &&
+        (hdr_mode == SNAPPY_HDR_EVERY_UNIT || (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0))) {
         const uint64_t expect = hdr_mode == SNAPPY_HDR_EVERY_UNIT ? want : header_value;
         const uint32_t o = (uint32_t)(c0 - B);
         uint64_t v = 0;
@@ -1544,8 +1645,54 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_de
             v |= (uint64_t)(byte & 0x7F) << (7 * k);
             if (!(byte & 0x80)) { done = true; k++; break; }
         }
-        if (!done || v != expect) st = SNAPPY_ST_HEADER;
+        if (!done || v != expect || skip0) st = SNAPPY_ST_HEADER;
         ip = k;
+    }
+
+    // ---- the unit starts inside the element at c0: resume it
+    if (st == SNAPPY_ST_OK && skip0) {
+        const uint32_t o = (uint32_t)(c0 - B);  // < 4
+        const uint64_t v = (((uint64_t)WDW(1) << 32) | WDW(0)) >> (8 * o);  // tag + 4 bytes
+        const uint32_t tag = (uint32_t)v & 0xFF, t = tag & 3, m = tag >> 2;
+        uint32_t hl, off = 0;
+        uint64_t len;
+        if (t == 0) {
+            const uint32_t k = m >= 60 ? m - 59 : 0;
+            hl = 1 + k;
+            len = (k ? ((v >> 8) & ((1ull << (8 * k)) - 1)) : m) + 1ull;
+        } else if (t == 1) {
+            hl = 2;
+            len = (m & 7) + 4;
+            off = ((tag >> 5) << 8) | ((uint32_t)(v >> 8) & 0xFF);
+        } else {
+            hl = t == 2 ? 3 : 5;
+            len = m + 1;
+            off = (uint32_t)(v >> 8) & (t == 2 ? 0xFFFFu : 0xFFFFFFFFu);
+        }
+        const uint64_t size = t == 0 ? hl + len : hl;
+        if (skip0 >= len || size > clen) {
+            st = SNAPPY_ST_TRUNCATED;
+        } else {
+            const uint64_t r = len - skip0;
+            const uint32_t k = r < want ? (uint32_t)r : want;
+            if (t == 0) {
+                k4_literal_hbm(comp + c0 + hl + skip0, k, 0, ob, M, dst, lane);
+                F = k;
+            } else if (off == 0 || (uint64_t)off + skip0 > base) {
+                st = SNAPPY_ST_OFFSET;
+            } else if constexpr (!BACK) {
+                st = SNAPPY_ST_DEFER;
+            } else {
+                // byte j of the unit is copy byte j + skip0: out[-skip0 - off + (j + skip0) mod off],
+                // always before the unit
+                const int64_t s0 = -(int64_t)skip0 - (int64_t)off;
+                const int64_t s1 = s0 + (int64_t)(len < off ? len : off) - 1;
+                st = k4_wait(status, base + s0, base + (s1 < -1 ? s1 : -1), unit, lane, &done_lo);
+                if (st == SNAPPY_ST_OK && lane < k) ob[lane & M] = dst[s0 + (int64_t)((lane + skip0) % off)];
+            }
+            op = k;
+            ip = (uint32_t)size;
+        }
     }
 
 #ifdef SNAPPY_K4_STATS
@@ -1593,9 +1740,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_de
             const uint32_t k = m >= 60 ? m - 59 : 0;  // literal: extra length bytes
             const uint32_t b4 = (x0 >> 8) | (x1 << 24);
             const uint32_t lv = k == 0 ? m : (k == 4 ? b4 : (x0 >> 8) & ((1u << (8 * (k & 3))) - 1));
-            const uint32_t c1 = ((tag >> 5) << 8) | ((x0 >> 8) & 0xFF);
+            const uint32_t c1b = ((tag >> 5) << 8) | ((x0 >> 8) & 0xFF);
             olen = t == 0 ? lv + 1 : (t == 1 ? (m & 7) + 4 : m + 1);  // garbage lengths are clamped below
-            info = t == 0 ? 1 + k : (t == 1 ? c1 : (t == 2 ? (x0 >> 8) & 0xFFFF : b4));
+            info = t == 0 ? 1 + k : (t == 1 ? c1b : (t == 2 ? (x0 >> 8) & 0xFFFF : b4));
             size = t == 0 ? 1 + k + lv + 1 : (t == 1 ? 2 : (t == 2 ? 3 : 5));
         }
         K4STAMP(tb);
@@ -1626,7 +1773,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_de
         const uint32_t pg = pos < 64 ? pos : 0;
         const uint32_t e_t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pg << 2), (int)t);
         const uint32_t e_size = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pg << 2), (int)size);
-        const uint32_t e_len = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pg << 2), (int)olen);
+        uint32_t e_len = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pg << 2), (int)olen);
         const uint32_t e_info = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pg << 2), (int)info);
         // exclusive prefix sums of compressed sizes and output lengths over
         // the batch (64-bit safe: garbage past E is zeroed)
@@ -1635,18 +1782,52 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_de
         const uint32_t in_off = wave_excl_scan32(live ? e_size : 0, &tot_in);  // E <= 32
         const uint32_t out_off = wave_excl_scan32(live ? e_len : 0, &tot_out);
         // validity in stream order: stop at the first element that runs past the
-        // unit (truncated / overrun), reaches before the unit start, or past want
+        // unit (truncated / overrun), reaches before the stream start, or needs
+        // an earlier unit's bytes (pass 1: DEFER); an element running past the
+        // unit's end is cut there when the index says the next unit resumes it
         const uint32_t e_ip = ip + in_off, e_op = op + out_off;
         int32_t e_err = SNAPPY_ST_OK;
-        if (e_op >= want) e_err = 1;  // done before this element: not an error
-        else if (e_size > clen - e_ip) e_err = SNAPPY_ST_TRUNCATED;
-        else if (e_len > want - e_op) e_err = SNAPPY_ST_OVERRUN;
-        else if (e_t != 0 && (e_info == 0 || e_info > e_op)) e_err = SNAPPY_ST_OFFSET;
+        bool e_back = false;
+        if constexpr (BACK) {
+            if (e_op >= want) {
+                e_err = 1;  // done before this element: not an error
+            } else if (e_size > clen - e_ip) {
+                e_err = SNAPPY_ST_TRUNCATED;
+            } else {
+                if (e_len > want - e_op) {
+                    if (e_ip != tail_ip) e_err = SNAPPY_ST_OVERRUN;
+                    e_len = want - e_op;
+                }
+                if (e_err == SNAPPY_ST_OK && e_t != 0 && (e_info == 0 || e_info > e_op)) {
+                    if (e_info == 0 || e_info - e_op > back_lim) e_err = SNAPPY_ST_OFFSET;
+                    else e_back = true;
+                }
+            }
+        } else {
+            if (e_op >= want) e_err = 1;  // done before this element: not an error
+            else if (e_size > clen - e_ip) e_err = SNAPPY_ST_TRUNCATED;
+            else if (e_t != 0 && (e_info == 0 || e_info > e_op)) e_err = e_info ? SNAPPY_ST_DEFER : SNAPPY_ST_OFFSET;
+            else if (e_len > want - e_op) e_err = kK4Tail;
+        }
         const uint64_t badm = __ballot(live && e_err != SNAPPY_ST_OK);
         uint32_t nexec = E;
         if (badm) {
             nexec = (uint32_t)__builtin_ctzll(badm);
-            const int32_t er = __builtin_amdgcn_readlane(e_err, nexec);
+            int32_t er = __builtin_amdgcn_readlane(e_err, nexec);
+            if (!BACK && er == kK4Tail) {
+                // the element runs past the unit's end: legal when the index says
+                // the next unit resumes it (entry u+1 re-read here, off the loop state)
+                const uint32_t t_ip = rfl(tail_lds[0]), t_op = rfl(tail_lds[1]);
+                const uint32_t kip = __builtin_amdgcn_readlane(e_ip, nexec);
+                const uint32_t kop = __builtin_amdgcn_readlane(e_op, nexec);
+                er = SNAPPY_ST_OVERRUN;
+                if (kip == t_ip && kop == t_op) {  // run it: op_end / op / the literal length are cut at want below
+                    er = 1;
+                    nexec++;
+                }
+            }
+            // pass 1: DEFER (a copy into an earlier unit) is final for a STREAMS
+            // unit (its own stream): the host reports it as SNAPPY_AMD_ERR_OFFSET
             if (er != 1) st = er;
         }
         K4STAMP(tc);
@@ -1658,31 +1839,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_de
             const uint32_t k = (uint32_t)__builtin_ctzll(longm);
             if (k == 0) {
                 nexec = 1;
-                const uint32_t kl = __builtin_amdgcn_readlane(e_len, 0);
                 const uint32_t kop = __builtin_amdgcn_readlane(e_op, 0);
+                const uint32_t kl0 = __builtin_amdgcn_readlane(e_len, 0);
+                const uint32_t kl = kl0 < want - kop ? kl0 : want - kop;  // a tail element ends at want
                 const uint32_t kip = __builtin_amdgcn_readlane(e_ip, 0);
                 const uint32_t ki = __builtin_amdgcn_readlane(e_info, 0);
-                const uint8_t *lsrc = comp + c0 + kip + ki;
-                // everything before the literal goes out first; the literal is
-                // written to HBM and to the ring (later copies read its tail)
+                // everything before the literal goes out first
                 k4_flush(ob, M, dst, F, kop, lane);
-#pragma unroll 1
-                for (uint32_t b = 0; b < kl; b += 256) {
-                    uint8_t v[4];
-#pragma unroll
-                    for (int m = 0; m < 4; m++) {
-                        const uint32_t jj = b + 64 * m + lane;
-                        v[m] = jj < kl ? lsrc[jj] : 0;
-                    }
-#pragma unroll
-                    for (int m = 0; m < 4; m++) {
-                        const uint32_t jj = b + 64 * m + lane;
-                        if (jj < kl) {
-                            ob[(kop + jj) & M] = v[m];
-                            dst[kop + jj] = v[m];
-                        }
-                    }
-                }
+                k4_literal_hbm(comp + c0 + kip + ki, kl, kop, ob, M, dst, lane);
                 F = kop + kl;
             } else {
                 nexec = k;
@@ -1698,8 +1862,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_de
             const uint64_t over = __ballot(ring < want && lane < nexec && lane > 0 &&
                                            op + out_off + e_len - F > ring - 64);
             if (over) nexec = (uint32_t)__builtin_ctzll(over);
-            const uint32_t op_end = op + __builtin_amdgcn_readlane(out_off, nexec - 1) +
-                                    __builtin_amdgcn_readlane(e_len, nexec - 1);
+            if constexpr (BACK) {
+                // copies reading earlier units: wait until those bytes are in HBM
+                uint64_t bm = __ballot(e_back && lane < nexec);
+                if (bm) {
+                    int64_t lo_s = INT64_MAX, hi_s = INT64_MIN;
+                    while (bm) {
+                        const uint32_t k = (uint32_t)__builtin_ctzll(bm);
+                        bm &= bm - 1;
+                        const int64_t s = (int64_t)(uint32_t)__builtin_amdgcn_readlane(e_op, k) -
+                                          (int64_t)(uint32_t)__builtin_amdgcn_readlane(e_info, k);
+                        const uint32_t kl = __builtin_amdgcn_readlane(e_len, k);
+                        const uint32_t ki = __builtin_amdgcn_readlane(e_info, k);
+                        const int64_t h = s + (int64_t)(kl < ki ? kl : ki) - 1;
+                        lo_s = s < lo_s ? s : lo_s;
+                        hi_s = h > hi_s ? h : hi_s;
+                    }
+                    if (hi_s > -1) hi_s = -1;
+                    st = k4_wait(status, base + lo_s, base + hi_s, unit, lane, &done_lo);
+                    if (st != SNAPPY_ST_OK) nexec = 0;
+                }
+            }
+        }
+        if (nexec && !(longm && (longm & 1))) {
+            uint32_t op_end = op + __builtin_amdgcn_readlane(out_off, nexec - 1) +
+                              __builtin_amdgcn_readlane(e_len, nexec - 1);
+            op_end = op_end < want ? op_end : want;  // a tail element ends at want
             // ring slots below lo were overwritten (or are being): read those from HBM
             const uint32_t lo = op_end > ring ? op_end - ring : 0;
             const bool ex = lane < nexec;
@@ -1748,14 +1936,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_de
                     const uint32_t qd = (uint32_t)((float)d * r + 0.0001f);
                     d -= qd * f_in;
                 }
-                const uint32_t src = (f_op & 0x7FFFFFFFu) - f_in + d;
+                const SrcT src = (SrcT)(f_op & 0x7FFFFFFFu) - (SrcT)f_in + (SrcT)d;
                 bool pend = o < op_end;
                 uint64_t written = 0;
                 for (;;) {
-                    const bool rdy = pend && (lit || src < P || ((written >> ((src - P) & 63)) & 1));
+                    const bool rdy = pend && (lit || src < (SrcT)P || ((written >> ((uint32_t)(src - (SrcT)P) & 63)) & 1));
                     if (rdy) {
                         uint8_t v = lb;
-                        if (!lit) v = src >= lo ? ob[src & M] : dst[src];
+                        if (!lit) v = src >= (SrcT)lo ? ob[(uint32_t)src & M] : dst[src];
                         ob[o & M] = v;
                     }
                     written |= __ballot(rdy);
@@ -1776,17 +1964,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_de
         sg1 += tc - tb;
         sg2 += td - tc;
         n_batch++;
-#endif
-#ifdef SNAPPY_K4_STATS
         n_el += nexec;
 #endif
         if (nexec) {
             ip += __builtin_amdgcn_readlane(in_off, nexec - 1) + __builtin_amdgcn_readlane(e_size, nexec - 1);
             op += __builtin_amdgcn_readlane(out_off, nexec - 1) + __builtin_amdgcn_readlane(e_len, nexec - 1);
+            op = op < want ? op : want;
             if (op - F >= 2048) {
                 const uint32_t T = op & ~1023u;
                 k4_flush(ob, M, dst, F, T, lane);
                 F = T;
+                if constexpr (BACK) k4_publish(status, u, SNAPPY_ST_DEFER + (int32_t)F, lane);
             }
         } else if (st == SNAPPY_ST_OK && op < want) {
             st = SNAPPY_ST_TRUNCATED;  // no progress possible
@@ -1810,9 +1998,38 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_de
     __syncthreads();
 
     k4_flush(ob, M, dst, F, op < want ? op : want, lane);
-    if (lane == 0) status[u] = st;
+    if constexpr (BACK) {
+        k4_publish(status, u, st, lane);
+    } else {
+        if (lane == 0) status[u] = st;
+        // status[units + 1] = pass 2 has work (status[units] is pass 2's ticket counter)
+        if (st == SNAPPY_ST_DEFER && lane == 0) status[gridDim.x + 1] = 1;
+    }
 }
 
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_decompress_units(
+    const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets, uint64_t n, uint32_t unit,
+    uint32_t hdr_mode, uint64_t header_value, uint32_t ring, uint32_t allow_back, uint8_t *__restrict__ out,
+    int32_t *__restrict__ status)
+{
+    k4_body<false>(comp, offsets, n, unit, hdr_mode, header_value, ring, allow_back, out, status, blockIdx.x);
+}
+
+__global__ __launch_bounds__(64) void k4_decompress_back(const uint8_t *__restrict__ comp,
+                                                         const uint64_t *__restrict__ offsets, uint64_t n,
+                                                         uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
+                                                         uint32_t ring, uint8_t *__restrict__ out,
+                                                         int32_t *__restrict__ status)
+{
+    // status[units + 1] == 0: pass 1 deferred nothing (the common case: every wave leaves at once)
+    if (*reinterpret_cast<const volatile int32_t *>(status + gridDim.x + 1) == 0) return;
+    // tickets in dispatch order: a unit only ever waits for lower tickets
+    uint32_t tk = 0;
+    if (threadIdx.x == 0) tk = atomicAdd(reinterpret_cast<uint32_t *>(status + gridDim.x), 1u);
+    const uint32_t u = __builtin_amdgcn_readfirstlane(tk);
+    if (status[u] != SNAPPY_ST_DEFER) return;
+    k4_body<true>(comp, offsets, n, unit, hdr_mode, header_value, ring, 1u, out, status, u);
+}
 // ---------------------------------------------------------------------------
 // K5: block index of a SINGLE-layout stream (one wave).  The stream is
 // walked through a 512-byte register window (two coalesced dword loads per
@@ -1868,6 +2085,7 @@ __global__ __launch_bounds__(64) void k5_index_stream(const uint8_t *__restrict_
     unit = 1;
     while (st == SNAPPY_ST_OK && op < N) {
         if (ip >= clen) { st = SNAPPY_ST_TRUNCATED; break; }
+        const uint64_t x = ip;  // element start
         const uint32_t tag = fetch(ip);
         uint64_t len;
         switch (tag & 3) {
@@ -1890,12 +2108,16 @@ __global__ __launch_bounds__(64) void k5_index_stream(const uint8_t *__restrict_
         }
         if (st != SNAPPY_ST_OK) break;
         if (ip > clen) { st = SNAPPY_ST_TRUNCATED; break; }
-        // element [op, op+len) must not straddle a 65,536 boundary
-        const uint64_t next_boundary = unit * SNAPPY_BLOCK;
-        if (op < next_boundary && op + len > next_boundary && next_boundary < N) {
-            st = SNAPPY_ST_UNSUPPORTED;
-            break;
+        // boundaries strictly inside [op, op+len): straddle entries (element
+        // start | bytes of it before the boundary << 40)
+        while (unit * SNAPPY_BLOCK < op + len && unit * SNAPPY_BLOCK < N) {
+            const uint64_t skip = unit * SNAPPY_BLOCK - op;
+            if ((skip >> 24) || (x >> 40)) { st = SNAPPY_ST_UNSUPPORTED; break; }
+            if (lane == 0) offsets[unit] = x | (skip << 40);
+            unit++;
         }
+        if (st != SNAPPY_ST_OK) break;
+        const uint64_t next_boundary = unit * SNAPPY_BLOCK;
         op += len;
         if (op == next_boundary && op < N) {
             if (lane == 0) offsets[unit] = ip;
@@ -2121,11 +2343,17 @@ __global__ __launch_bounds__(64) void k5c_mark(const uint8_t *__restrict__ comp,
                 st = SNAPPY_ST_TRUNCATED;
                 break;
             }
-            const uint64_t nb = (op / SNAPPY_BLOCK + 1) * SNAPPY_BLOCK;  // element must not straddle a block
-            if (op + len > nb && nb < N) {
-                st = SNAPPY_ST_UNSUPPORTED;
-                break;
+            // boundaries strictly inside the element: straddle entries
+            for (uint64_t nb = (op / SNAPPY_BLOCK + 1) * SNAPPY_BLOCK; nb < op + len && nb < N; nb += SNAPPY_BLOCK) {
+                const uint64_t skip = nb - op;
+                if ((skip >> 24) || (x >> 40)) {
+                    st = SNAPPY_ST_UNSUPPORTED;
+                    break;
+                }
+                const uint64_t u = nb / SNAPPY_BLOCK;
+                if (lane == 0 && u < max_units) offsets[u] = x | (skip << 40);
             }
+            if (st != SNAPPY_ST_OK) break;
             op += len;
             x += size;
             if (op > N) {

@@ -33,6 +33,7 @@ ERR_CAPACITY = -6
 ERR_DEVICE = -7
 ERR_IO = -8
 ERR_UNSUPPORTED = -9
+ERR_TIMEOUT = -10
 
 BLOCK = 65536
 SINGLE = 0
@@ -49,6 +50,7 @@ _NAMES = {
     ERR_DEVICE: "HIP device error",
     ERR_IO: "I/O error",
     ERR_UNSUPPORTED: "unsupported",
+    ERR_TIMEOUT: "block dependency wait timed out",
 }
 
 # every function include/*.h declares, with its ctypes signature

@@ -11,6 +11,8 @@ Entries:
   * the Appendix A.4 edge matrix (sizes x data kinds);
   * the reference decoder on hand-built streams using elements the reference
     compressor never emits (copy-4, 4-byte literal lengths, overlaps);
+  * cross-block decoder vectors (elements straddling 65,536-byte blocks,
+    copies into earlier blocks; hand-built and seeded random foreign streams);
   * the reference's own varint KATs (src/test_varint.c:27-35);
   * the 32 KiB-stream layout of BASELINE.json configs[1] on a 32 MiB sample.
 Usage: python oracle/gen_golden.py
@@ -28,7 +30,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 sys.path.insert(0, os.path.join(ROOT, "lightweight-snappy_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 import datagen  # noqa: E402
+import golden_inputs  # noqa: E402
 import oracle  # noqa: E402
 
 GOLD = os.path.join(ROOT, "tests", "golden")
@@ -140,14 +144,44 @@ def main() -> None:
     dec("copy1_hi_offset", bytes([0x8D, 0x08, 61 << 2, 0xFF, 0x03]) + bytes((i * 7) & 0xFF for i in range(1024))
         + bytes([(3 << 5) | ((8 - 4) << 2) | 1, 0xE8]) + bytes([((5 - 1) << 2) | 2, 0x00, 0x04]), 1037)
 
+    # --- cross-block decoder vectors: streams another encoder could write, whose
+    # elements straddle 65,536-byte output blocks and whose copies reach into
+    # earlier blocks (up to the reference's 131,072 limit,
+    # src/snappy_decompression.c:262); the streams are rebuilt from their specs
+    # by tests/golden_inputs.py, only hashes are committed
+    xblock = []
+
+    def xvec(name: str, ops: list | None = None, rnd: dict | None = None):
+        if rnd is not None:
+            ops = golden_inputs.random_ops(rnd["seed"], rnd["n_out"], rnd["max_off"])
+        stream = golden_inputs.build_stream(ops)
+        n_out = golden_inputs.uncompressed_length(stream)
+        out = oracle.ref_decompress(stream, n_out)
+        assert len(out) == n_out, name
+        assert oracle.decompress(stream) == out, f"oracle differs from the reference on {name}"
+        e = {"name": name, "stream_len": len(stream), "stream_sha256": sha(stream), "out_len": n_out,
+             "out_sha256": sha(out)}
+        if rnd is not None:
+            e["random"] = rnd
+        else:
+            e["ops"] = ops
+        xblock.append(e)
+
+    for name, ops in golden_inputs.decoder_vector_ops().items():
+        xvec(name, ops=ops)
+    for seed, n_out, max_off in [(1, 300_000, 131072), (2, 500_000, 131072), (3, 700_000, 65535),
+                                 (4, 1_000_000, 131072), (5, 262_144, 131072), (6, 2_000_000, 131072)]:
+        xvec(f"foreign_random_{seed}", rnd={"seed": seed, "n_out": n_out, "max_off": max_off})
+
     varint_kats = [{"n": 127, "hex": "7f"}, {"n": 227, "hex": "e301"}, {"n": 16384, "hex": "808001"},
                    {"n": 1000000, "hex": "c0843d"}, {"n": 1 << 30, "hex": "8080808004"}, {"n": 32768, "hex": "808002"}]
 
     gold = {"generator": "oracle/gen_golden.py", "reference": "tturturiello/lightweight-snappy (oracle/_ref)",
-            "entries": entries, "streams_32k": streams, "decoder_vectors": dec_vectors, "varint": varint_kats}
+            "entries": entries, "streams_32k": streams, "decoder_vectors": dec_vectors,
+            "xblock_vectors": xblock, "varint": varint_kats}
     with open(os.path.join(GOLD, "golden.json"), "w") as f:
         json.dump(gold, f, indent=1)
-    print(f"wrote {len(entries)} entries, {len(dec_vectors)} decoder vectors")
+    print(f"wrote {len(entries)} entries, {len(dec_vectors)} decoder vectors, {len(xblock)} cross-block vectors")
 
 
 if __name__ == "__main__":

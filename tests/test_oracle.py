@@ -9,7 +9,7 @@ import pytest
 
 import datagen
 import oracle
-from golden_inputs import make_input
+from golden_inputs import build_stream, make_input, random_ops
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HAVE_REF = os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libsnappy_ref.so"))
@@ -92,3 +92,29 @@ def test_oracle_matches_reference_live():
         if trial % 5 == 0 and n > 100:  # mixed text/random splices
             data = data[: n // 2] + datagen.make("R", n - n // 2, trial).tobytes()
         assert oracle.compress(data) == oracle.ref_compress(data)
+
+
+def _xblock_stream(v):
+    if "random" in v:
+        r = v["random"]
+        return build_stream(random_ops(r["seed"], r["n_out"], r["max_off"]))
+    return build_stream(v["ops"])
+
+
+def test_xblock_vectors(golden):
+    # streams whose elements straddle 65,536-byte blocks and whose copies reach
+    # into earlier blocks: the oracle decodes them exactly as the reference did
+    assert len(golden["xblock_vectors"]) >= 15
+    for v in golden["xblock_vectors"]:
+        stream = _xblock_stream(v)
+        assert len(stream) == v["stream_len"] and sha(stream) == v["stream_sha256"], v["name"]
+        out = oracle.decompress(stream)
+        assert len(out) == v["out_len"] and sha(out) == v["out_sha256"], v["name"]
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="reference build only in the build container")
+def test_oracle_decoder_matches_reference_on_foreign_streams():
+    for seed in range(100, 112):
+        stream = build_stream(random_ops(seed, 150_000 + 37_000 * (seed % 5), 131072))
+        n = len(oracle.decompress(stream))
+        assert oracle.decompress(stream) == oracle.ref_decompress(stream, n)

@@ -19,8 +19,6 @@ struct snappy_amd_ctx {
     int device = 0;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
-    uint8_t *scratch = nullptr;
-    size_t scratch_cap = 0;
     uint32_t *sizes = nullptr;
     size_t sizes_cap = 0;
     uint2 *tokens = nullptr;
@@ -61,7 +59,6 @@ static int grow(void **ptr, size_t *cap, size_t need)
     return SNAPPY_AMD_OK;
 }
 
-static size_t k1_lds_bytes(uint32_t unit) { return 8192 + ((unit + 15) & ~15u); }
 // K4 output ring: the whole unit when it fits 4 KiB, else a 4 KiB ring (the
 // wave-slot limit, 28 units per CU at 85 SGPRs, binds before LDS does; copies
 // reaching further back read HBM).  SNAPPY_AMD_K4_RING overrides (power of
@@ -101,9 +98,7 @@ int snappy_amd_create(int device, snappy_amd_ctx **out)
         return SNAPPY_AMD_ERR_DEVICE;
     }
     for (int i = 0; i < 5; i++) (void)hipEventCreate(&c->ev[i]);
-    // K1/K4 use up to 72 KiB / 132 KiB of dynamic LDS with 65,536-byte units
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k1_compress_units),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    // K4's ring may be raised to 64 KiB (SNAPPY_AMD_K4_RING)
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k4_decompress_units),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k4_decompress_back),
@@ -117,7 +112,7 @@ void snappy_amd_destroy(snappy_amd_ctx *c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void *bufs[] = {c->scratch, c->sizes, c->tokens, c->ntok, c->seg_off, c->status, c->total, c->k5res,
+    void *bufs[] = {c->sizes, c->tokens, c->ntok, c->seg_off, c->status, c->total, c->k5res,
                     c->d_a, c->d_b, c->d_idx, c->k5buf};
     for (void *b : bufs) if (b) (void)hipFree(b);
     if (c->h_total) (void)hipHostFree(c->h_total);
@@ -199,63 +194,41 @@ static int compress_impl(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t
     }
     const size_t units = (n + unit - 1) / unit;
     int rc;
-    if (!getenv("SNAPPY_AMD_FORCE_LDS_K1")) {
-        // register-resident match finder -> tokens; scan; emit in place
-        const uint32_t tok_cap = unit / 4 + 2;
-        if ((rc = grow(reinterpret_cast<void **>(&c->tokens), &c->tokens_cap,
-                       units * tok_cap * sizeof(uint2) + units * 4 * sizeof(uint64_t))))
-            return rc;
-        if ((rc = grow(reinterpret_cast<void **>(&c->ntok), &c->ntok_cap, units * sizeof(uint32_t)))) return rc;
-        if ((rc = grow(reinterpret_cast<void **>(&c->sizes), &c->sizes_cap, units * sizeof(uint32_t)))) return rc;
-        // segments per unit: tokens 0..ntok (the tail literal is token ntok <= tok_cap - 1)
-        const uint32_t segs = (tok_cap + SNAPPY_K2_SEG - 1) / SNAPPY_K2_SEG;
-        if ((rc = grow(reinterpret_cast<void **>(&c->seg_off), &c->seg_off_cap, units * segs * sizeof(uint32_t))))
-            return rc;
-        const uint32_t hm = hdr_mode_of(layout, flags);
-        if (c->timing) (void)hipEventRecord(c->ev[0], c->stream);
-        // units <= 32 KiB: unit in VGPRs (3 waves/SIMD); 64 KiB blocks: VGPRs + AGPRs (1 wave/SIMD)
-        // SNAPPY_K1R_DYNLDS=<bytes>: occupancy experiments (extra dynamic LDS per unit)
-        const char *dyn = getenv("SNAPPY_K1R_DYNLDS");
-        const uint32_t dyn_lds = dyn ? (uint32_t)atoi(dyn) : 0;
-        if (unit <= SNAPPY_K1R_MAX_UNIT)
-            hipLaunchKernelGGL(k1r_match_units, dim3((uint32_t)units), dim3(64), dyn_lds, c->stream,
-                               static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens,
-                               tok_cap, c->ntok, c->sizes, c->seg_off, segs);
-        else
-            hipLaunchKernelGGL(k1r_match_units64, dim3((uint32_t)units), dim3(64), 0, c->stream,
-                               static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens,
-                               tok_cap, c->ntok, c->sizes, c->seg_off, segs);
-        HIP_OK(hipGetLastError());
-        if (c->timing) (void)hipEventRecord(c->ev[1], c->stream);
-        hipLaunchKernelGGL(k3_scan, dim3(1), dim3(1024), 0, c->stream, c->sizes, (uint64_t)units, d_offsets, c->total);
-        // K1r wrote the sizes and segment offsets; K2: a few waves per unit, each taking
-        // every SNAPPY_K2_WAVES-th segment (text fills ~12 segments of 32 KiB units)
-        hipLaunchKernelGGL(k2_emit_units, dim3((uint32_t)units, segs < SNAPPY_K2_WAVES ? segs : SNAPPY_K2_WAVES), dim3(64), 0, c->stream,
-                           static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens, tok_cap,
-                           c->ntok, c->seg_off, segs, d_offsets, static_cast<uint8_t *>(d_out));
-        HIP_OK(hipGetLastError());
-        if (c->timing) (void)hipEventRecord(c->ev[2], c->stream);
-        goto done;
-    }
-    {
-    const uint64_t stride = unit_stride(unit);
-    if ((rc = grow(reinterpret_cast<void **>(&c->scratch), &c->scratch_cap, units * stride))) return rc;
+    // register-resident match finder -> tokens; scan; emit in place
+    const uint32_t tok_cap = unit / 4 + 2;
+    if ((rc = grow(reinterpret_cast<void **>(&c->tokens), &c->tokens_cap,
+                   units * tok_cap * sizeof(uint2) + units * 4 * sizeof(uint64_t))))
+        return rc;
+    if ((rc = grow(reinterpret_cast<void **>(&c->ntok), &c->ntok_cap, units * sizeof(uint32_t)))) return rc;
     if ((rc = grow(reinterpret_cast<void **>(&c->sizes), &c->sizes_cap, units * sizeof(uint32_t)))) return rc;
-    const uint32_t vec_ok = ((reinterpret_cast<uintptr_t>(d_in) | unit) & 15) == 0;
+    // segments per unit: tokens 0..ntok (the tail literal is token ntok <= tok_cap - 1)
+    const uint32_t segs = (tok_cap + SNAPPY_K2_SEG - 1) / SNAPPY_K2_SEG;
+    if ((rc = grow(reinterpret_cast<void **>(&c->seg_off), &c->seg_off_cap, units * segs * sizeof(uint32_t))))
+        return rc;
+    const uint32_t hm = hdr_mode_of(layout, flags);
     if (c->timing) (void)hipEventRecord(c->ev[0], c->stream);
-    hipLaunchKernelGGL(k1_compress_units, dim3((uint32_t)units), dim3(64), k1_lds_bytes(unit), c->stream,
-                       static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hdr_mode_of(layout, flags), header_value,
-                       vec_ok,
-                       c->scratch, stride, c->sizes);
+    // units <= 32 KiB: unit in VGPRs (3 waves/SIMD); 64 KiB blocks: VGPRs + AGPRs (1 wave/SIMD)
+    // SNAPPY_K1R_DYNLDS=<bytes>: occupancy experiments (extra dynamic LDS per unit)
+    const char *dyn = getenv("SNAPPY_K1R_DYNLDS");
+    const uint32_t dyn_lds = dyn ? (uint32_t)atoi(dyn) : 0;
+    if (unit <= SNAPPY_K1R_MAX_UNIT)
+        hipLaunchKernelGGL(k1r_match_units, dim3((uint32_t)units), dim3(64), dyn_lds, c->stream,
+                           static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens,
+                           tok_cap, c->ntok, c->sizes, c->seg_off, segs);
+    else
+        hipLaunchKernelGGL(k1r_match_units64, dim3((uint32_t)units), dim3(64), 0, c->stream,
+                           static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens,
+                           tok_cap, c->ntok, c->sizes, c->seg_off, segs);
     HIP_OK(hipGetLastError());
     if (c->timing) (void)hipEventRecord(c->ev[1], c->stream);
     hipLaunchKernelGGL(k3_scan, dim3(1), dim3(1024), 0, c->stream, c->sizes, (uint64_t)units, d_offsets, c->total);
-    hipLaunchKernelGGL(k3_gather, dim3((uint32_t)units), dim3(256), 0, c->stream, c->scratch, stride, c->sizes,
-                       d_offsets, static_cast<uint8_t *>(d_out));
+    // K1r wrote the sizes and segment offsets; K2: a few waves per unit, each taking
+    // every SNAPPY_K2_WAVES-th segment (text fills ~12 segments of 32 KiB units)
+    hipLaunchKernelGGL(k2_emit_units, dim3((uint32_t)units, segs < SNAPPY_K2_WAVES ? segs : SNAPPY_K2_WAVES), dim3(64), 0, c->stream,
+                       static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens, tok_cap,
+                       c->ntok, c->seg_off, segs, d_offsets, static_cast<uint8_t *>(d_out));
     HIP_OK(hipGetLastError());
     if (c->timing) (void)hipEventRecord(c->ev[2], c->stream);
-    }
-done:
     if (out_len) {
         HIP_OK(hipMemcpyAsync(c->h_total, c->total, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
         HIP_OK(hipStreamSynchronize(c->stream));
@@ -288,7 +261,6 @@ static int decompress_launch(snappy_amd_ctx *c, const void *d_comp, const uint64
     if (layout != SNAPPY_AMD_SINGLE && layout != SNAPPY_AMD_STREAMS) return SNAPPY_AMD_ERR_ARG;
     const uint32_t unit = layout == SNAPPY_AMD_SINGLE ? SNAPPY_AMD_BLOCK : chunk;
     if (unit == 0 || unit > SNAPPY_AMD_BLOCK) return SNAPPY_AMD_ERR_ARG;
-    if (reinterpret_cast<uintptr_t>(d_comp) & 3) return SNAPPY_AMD_ERR_ARG;
     HIP_OK(hipSetDevice(c->device));
     c->last_units = 0;
     if (n == 0) return SNAPPY_AMD_OK;
@@ -306,14 +278,17 @@ static int decompress_launch(snappy_amd_ctx *c, const void *d_comp, const uint64
     const uint32_t ring = k4_ring_bytes(unit);
     const uint32_t hm = hdr_mode_of(layout, flags);
     // dynamic LDS: the ring + 16 bytes of per-unit scalars
-    hipLaunchKernelGGL(k4_decompress_units, dim3((uint32_t)units), dim3(64), ring + 16, c->stream,
-                       static_cast<const uint8_t *>(d_comp), d_offsets, (uint64_t)n, unit, hm, header_value, ring,
-                       allow_back, static_cast<uint8_t *>(d_out), c->status);
+    // the kernel reads aligned dwords: pass the stream as an aligned base + bias
+    const uint32_t bias = (uint32_t)(reinterpret_cast<uintptr_t>(d_comp) & 3);
+    const uint8_t *comp = static_cast<const uint8_t *>(d_comp) - bias;
+    hipLaunchKernelGGL(k4_decompress_units, dim3((uint32_t)units), dim3(64), ring + 16, c->stream, comp, d_offsets,
+                       (uint64_t)n, unit, hm, header_value, ring, allow_back, bias, static_cast<uint8_t *>(d_out),
+                       c->status);
     HIP_OK(hipGetLastError());
     if (allow_back) {
-        hipLaunchKernelGGL(k4_decompress_back, dim3((uint32_t)units), dim3(64), ring + 16, c->stream,
-                           static_cast<const uint8_t *>(d_comp), d_offsets, (uint64_t)n, unit, hm, header_value, ring,
-                           static_cast<uint8_t *>(d_out), c->status);
+        hipLaunchKernelGGL(k4_decompress_back, dim3((uint32_t)units), dim3(64), ring + 16, c->stream, comp,
+                           d_offsets, (uint64_t)n, unit, hm, header_value, ring, bias, static_cast<uint8_t *>(d_out),
+                           c->status);
         HIP_OK(hipGetLastError());
     }
     if (c->timing) (void)hipEventRecord(c->ev[4], c->stream);

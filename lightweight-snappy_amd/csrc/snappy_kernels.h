@@ -27,16 +27,6 @@
 
 namespace snappy_amd {
 
-// bytes of fixed-stride scratch per unit: worst-case element expansion plus
-// a 10-byte preamble, padded to 16 for aligned slot starts.
-__host__ __device__ inline uint64_t unit_stride(uint32_t unit)
-{
-    return ((uint64_t)unit + unit / 32 + 16 + 16 + 15) & ~15ull;
-}
-
-__global__ void k1_compress_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit, uint32_t hdr_mode,
-                                  uint64_t header_value, uint32_t vec_ok, uint8_t *__restrict__ scratch,
-                                  uint64_t stride, uint32_t *__restrict__ sizes);
 __global__ void k1r_match_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit, uint32_t hdr_mode,
                                 uint64_t header_value, uint2 *__restrict__ tokens, uint32_t tok_cap,
                                 uint32_t *__restrict__ ntok_out, uint32_t *__restrict__ sizes,
@@ -57,20 +47,20 @@ __global__ void k2_emit_units(const uint8_t *__restrict__ in, uint64_t n, uint32
 
 __global__ void k3_scan(const uint32_t *__restrict__ sizes, uint64_t count, uint64_t *__restrict__ offsets,
                         uint64_t *__restrict__ total);
-__global__ void k3_gather(const uint8_t *__restrict__ scratch, uint64_t stride, const uint32_t *__restrict__ sizes,
-                          const uint64_t *__restrict__ offsets, uint8_t *__restrict__ out);
+// K4: comp is 4-byte aligned, the stream starts at comp + bias (bias < 4).
 // K4 pass 1: every unit; allow_back = 1 for SINGLE-layout streams (straddling
 // elements and copies into earlier blocks are legal: such units end with
 // status SNAPPY_ST_DEFER, for pass 2, and set status[units + 1])
 __global__ void k4_decompress_units(const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets,
                                     uint64_t n, uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
-                                    uint32_t ring, uint32_t allow_back, uint8_t *__restrict__ out,
+                                    uint32_t ring, uint32_t allow_back, uint32_t bias, uint8_t *__restrict__ out,
                                     int32_t *__restrict__ status);
 // K4 pass 2: the DEFER units, in ticket order (status[units] = ticket counter,
 // status[units + 1] = pass 1's defer flag; both 0 before pass 1)
 __global__ void k4_decompress_back(const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets,
                                    uint64_t n, uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
-                                   uint32_t ring, uint8_t *__restrict__ out, int32_t *__restrict__ status);
+                                   uint32_t ring, uint32_t bias, uint8_t *__restrict__ out,
+                                   int32_t *__restrict__ status);
 constexpr uint32_t K5_CHUNK = 16384;  // == K5_S in the kernels
 __global__ void k5a_chunk_walk(const uint8_t *__restrict__ comp, uint64_t clen, uint64_t *__restrict__ X,
                                uint64_t *__restrict__ O);

@@ -2,20 +2,18 @@
 // block codec.  One wave64 per independent unit (a 65,536-byte block of a
 // single stream, or one <=65,536-byte stream of the STREAMS layout).
 //
-//   K1 k1_compress_units   per-unit LZ77 match finder + element emit
+//   K1r k1r_match_units(64) per-unit LZ77 match finder -> tokens
 //                          (reference: src/snappy_compression.c:384-403 and
-//                          helpers :61-165, :229-329)
-//   K3 k3_scan / k3_gather exclusive scan of unit sizes -> block index, then
-//                          compaction of the fixed-stride scratch into one
-//                          contiguous stream (replaces the per-block fwrite,
-//                          src/snappy_compression.c:334-336)
-//   K4 k4_decompress_units tag-dispatch decode of one unit into an LDS window
-//                          (src/snappy_decompression.c:290-333)
-//   K5 k5_index_stream     block index of a foreign single stream
+//                          helpers :61-72, :229-329)
+//   K3  k3_scan            exclusive scan of unit sizes -> block index
+//   K2  k2_emit_units      tokens -> Snappy elements at their final offsets
+//                          (:95-165; replaces the per-block fwrite :334-336)
+//   K4  k4_decompress_*    tag-dispatch decode, block-parallel
+//                          (src/snappy_decompression.c:290-363)
+//   K5  k5_* / k5a-d       block index of a foreign single stream
 //
-// Data layout in LDS (K1): [u16 hash table, 4096 entries][unit input bytes
-// + 16 zero pad].  The table holds block-relative positions; 0 is a valid
-// candidate, exactly as in the reference (snappy_compression.c:259-265).
+// The hash table holds block-relative positions; 0 is a valid candidate,
+// exactly as in the reference (snappy_compression.c:259-265).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <type_traits>
@@ -35,20 +33,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// Little-endian dword starting at byte q of a dword-aligned byte buffer.
-__device__ __forceinline__ uint32_t le32_at(const uint32_t *w, uint32_t q)
-{
-    const uint32_t a = w[q >> 2];
-    const uint32_t b = w[(q >> 2) + 1];
-    return __builtin_amdgcn_alignbyte(b, a, q & 3);
-}
-
-// Big-endian load of src/snappy_compression.c:239-241.
-__device__ __forceinline__ uint32_t be32_at(const uint32_t *w, uint32_t q)
-{
-    return __builtin_bswap32(le32_at(w, q));
-}
-
 __device__ __forceinline__ uint32_t varint_put(uint64_t v, uint8_t *out, uint32_t lane)
 {
     // every lane computes the same encoding; lanes < len store one byte each
@@ -63,75 +47,6 @@ __device__ __forceinline__ uint32_t varint_put(uint64_t v, uint8_t *out, uint32_
     return len;
 }
 
-// Literal element, src/snappy_compression.c:95-120: tag (len-1)<<2 for
-// len-1 < 60, else tag (59+k)<<2 followed by len-1 in k LE bytes.
-__device__ __forceinline__ uint32_t emit_literal(uint8_t *ob, uint32_t o, const uint8_t *inb, uint32_t start,
-                                                 uint32_t len, uint32_t lane)
-{
-    const uint32_t m = len - 1;
-    uint32_t hl, hdr;
-    if (m < 60) { hl = 1; hdr = m << 2; }
-    else if (m < 256) { hl = 2; hdr = (60u << 2) | (m << 8); }
-    else { hl = 3; hdr = (61u << 2) | (m << 8); }
-    const uint32_t total = hl + len;
-    for (uint32_t b = 0; b < total; b += 64) {
-        const uint32_t i = b + lane;
-        if (i < total) {
-            const uint32_t sh = (i < hl ? i : 0) * 8;
-            ob[o + i] = i < hl ? (uint8_t)(hdr >> sh) : inb[start + i - hl];
-        }
-    }
-    return o + total;
-}
-
-// Copy split 64/60 (src/snappy_compression.c:153-165) and piece encoding
-// (:131-145): copy-1 iff len < 12 && off < 2048, else copy-2; never copy-4.
-__device__ __forceinline__ uint32_t piece_bytes(uint32_t len, uint32_t off, uint32_t *nb)
-{
-    if (len < 12 && off < 2048) {
-        *nb = 2;
-        return ((((off >> 8) << 5) + ((len - 4) << 2) + 1) & 0xFF) | ((off & 0xFF) << 8);
-    }
-    *nb = 3;
-    return (((len - 1) << 2) | 2) | ((off & 0xFF) << 8) | (((off >> 8) & 0xFF) << 16);
-}
-
-__device__ __forceinline__ uint32_t emit_copy(uint8_t *ob, uint32_t o, uint32_t len, uint32_t off, uint32_t lane)
-{
-    if (len <= 64) {  // one piece: the common case
-        uint32_t nb;
-        const uint32_t v = piece_bytes(len, off, &nb);
-        if (lane < nb) ob[o + lane] = (uint8_t)(v >> (8 * lane));
-        return o + nb;
-    }
-    const uint32_t n64 = len > 68 ? (len - 68 + 63) >> 6 : 0;
-    const uint32_t rem = len - 64 * n64;
-    const uint32_t has60 = rem > 64 ? 1u : 0u;
-    const uint32_t last = has60 ? rem - 60 : rem;
-    const uint32_t offb = ((off & 0xFF) << 8) | (((off >> 8) & 0xFF) << 16);
-    const uint32_t c64 = 0xFEu | offb;  // ((64-1)<<2)|2
-    const uint32_t c60 = 0xEEu | offb;  // ((60-1)<<2)|2
-    uint32_t lastl;
-    const uint32_t lastb = piece_bytes(last, off, &lastl);
-    const uint32_t body = 3 * (n64 + has60);
-    const uint32_t total = body + lastl;
-    for (uint32_t b = 0; b < total; b += 64) {
-        const uint32_t i = b + lane;
-        if (i < total) {
-            uint32_t v;
-            if (i < body) {
-                const uint32_t piece = i / 3;
-                const uint32_t k = i - 3 * piece;
-                v = (piece < n64 ? c64 : c60) >> (8 * k);
-            } else {
-                v = lastb >> (8 * (i - body));
-            }
-            ob[o + i] = (uint8_t)v;
-        }
-    }
-    return o + total;
-}
-
 // Probe position of the k-th consecutive miss after (p, skip):
 // p_k = p + sum_{j<k} ((skip + j) >> 5) = p + F(skip + k) - F(skip), with
 // F(m) = sum_{i<m} (i >> 5) = 16 q (q - 1) + (m & 31) q, q = m >> 5.
@@ -139,160 +54,6 @@ __device__ __forceinline__ uint32_t skipsum(uint32_t m)
 {
     const uint32_t q = m >> 5;
     return 16 * q * (q - 1) + (m & 31) * q;
-}
-
-// row_shr:N inside 16-lane DPP rows; lanes with no source get 0xFFFFFFFF
-// (never equal to a 12-bit hash or to a position + 1).
-template <int N>
-__device__ __forceinline__ uint32_t shr(uint32_t v)
-{
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)v, 0x110 + N, 0xF, 0xF, false);
-}
-
-// Lane k (< W) conflicts with an earlier lane j of the window when its probe
-// would read a slot j writes (h_k in {h_j, a_j}) or when the two lanes would
-// write different positions into one slot in the same LDS instruction
-// (a_k in {a_j} or a_k == h_j with p_j != p_k - 1).  Only j = k - 1 can have
-// p_j == p_k - 1 (when its step is 1): `dup` carries that fact.
-template <int N>
-__device__ __forceinline__ bool conflict_step(uint32_t h, uint32_t a, bool dup)
-{
-    const uint32_t hs = shr<N>(h), as = shr<N>(a);
-    if constexpr (N == 1) return (h == hs) | (h == as) | (a == as) | ((a == hs) & !dup);
-    else return (h == hs) | (h == as) | (a == as) | (a == hs);
-}
-
-template <int W>
-__device__ __forceinline__ bool window_conflict(uint32_t h, uint32_t a, bool dup)
-{
-    bool c = false;
-    if constexpr (W > 1) c |= conflict_step<1>(h, a, dup);
-    if constexpr (W > 2) c |= conflict_step<2>(h, a, dup);
-    if constexpr (W > 3) c |= conflict_step<3>(h, a, dup);
-    if constexpr (W > 4) {
-        c |= conflict_step<4>(h, a, dup);
-        c |= conflict_step<5>(h, a, dup);
-        c |= conflict_step<6>(h, a, dup);
-        c |= conflict_step<7>(h, a, dup);
-    }
-    if constexpr (W > 8) {
-        c |= conflict_step<8>(h, a, dup);
-        c |= conflict_step<9>(h, a, dup);
-        c |= conflict_step<10>(h, a, dup);
-        c |= conflict_step<11>(h, a, dup);
-        c |= conflict_step<12>(h, a, dup);
-        c |= conflict_step<13>(h, a, dup);
-        c |= conflict_step<14>(h, a, dup);
-        c |= conflict_step<15>(h, a, dup);
-    }
-    return c;
-}
-
-// ---------------------------------------------------------------------------
-// K1: one wave per unit.  Control state (p, skip, literal start, output
-// cursor) is wave-uniform.  Each round speculates that the next W probes all
-// miss: lane k computes probe k's position in closed form, hashes, reads its
-// table slot and candidate bytes; a ballot finds the first lane that matches,
-// conflicts with an earlier lane of the window, or is past the block end.
-// Lanes before it are exact misses (their inserts are applied, collision-free
-// by construction); the match, if any, is exact too.  This reproduces the
-// reference's serial probe/insert order bit for bit while paying the LDS
-// round trips once per window instead of once per probe.
-// ---------------------------------------------------------------------------
-#ifndef SNAPPY_K1_WINDOW
-#define SNAPPY_K1_WINDOW 8
-#endif
-constexpr int kWin = SNAPPY_K1_WINDOW;
-
-__global__ __launch_bounds__(64) void k1_compress_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
-                                                        uint32_t hdr_mode, uint64_t header_value, uint32_t vec_ok,
-                                                        uint8_t *__restrict__ scratch, uint64_t stride,
-                                                        uint32_t *__restrict__ sizes)
-{
-    extern __shared__ uint32_t lds[];
-    uint16_t *table = reinterpret_cast<uint16_t *>(lds);
-    uint32_t *inw = lds + kTable / 2;
-    uint8_t *inb = reinterpret_cast<uint8_t *>(inw);
-
-    const uint32_t lane = threadIdx.x;
-    const uint32_t u = blockIdx.x;
-    const uint64_t base = (uint64_t)u * unit;
-    const uint32_t L = (uint32_t)((n - base) < unit ? (n - base) : unit);
-    const uint8_t *src = in + base;
-
-    // Stage the unit into LDS: 16 B per lane per step (1 KiB per wave op).
-    if (vec_ok) {
-        const uint32_t L16 = L & ~15u;
-        for (uint32_t i = lane * 16; i < L16; i += 1024)
-            *reinterpret_cast<u32x4 *>(inb + i) = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src + i));
-        for (uint32_t i = L16 + lane; i < L; i += 64) inb[i] = src[i];
-    } else {
-        for (uint32_t i = lane; i < L; i += 64) inb[i] = src[i];
-    }
-    for (uint32_t i = lane * 4; i < kTable / 2; i += 256) *reinterpret_cast<u32x4 *>(lds + i) = u32x4{0, 0, 0, 0};
-    __syncthreads();
-
-    uint8_t *ob = scratch + (uint64_t)u * stride;
-    uint32_t o = 0;
-    if (hdr_mode == SNAPPY_HDR_EVERY_UNIT) o = varint_put(L, ob, lane);
-    else if (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0) o = varint_put(header_value, ob, lane);
-
-    // set_htable_size, src/snappy_compression.c:198-204
-    uint32_t T = 256, lg = 8;
-    while (T < kTable && T < L) { T <<= 1; lg++; }
-    const uint32_t shift = 32 - lg;
-
-    uint32_t p = 1, skip = 33, lit = 0;  // start_new_literal + append_literal
-    while (!(L - p < (skip >> 5) + 15)) {  // is_block_end :229-232
-        // ---- speculative window: lane k = k-th probe if all earlier miss
-        const uint32_t sk = skip + lane;
-        const uint32_t pk = p + skipsum(sk) - skipsum(skip);
-        const bool valid = lane < (uint32_t)kWin && (int32_t)(L - pk) >= (int32_t)((sk >> 5) + 15);
-        const uint32_t q = valid ? pk - 1 : 0;
-        const uint32_t lo = inw[q >> 2], hi = inw[(q >> 2) + 1];
-        const uint64_t w8 = ((uint64_t)hi << 32) | lo;
-        const uint32_t prev = __builtin_bswap32((uint32_t)(w8 >> (8 * (q & 3))));
-        const uint32_t cur = __builtin_bswap32((uint32_t)(w8 >> (8 * (q & 3) + 8)));
-        const uint32_t h = (cur * kMul) >> shift;
-        const uint32_t a = (prev * kMul) >> shift;
-        const uint32_t cand = table[h];
-        // the previous lane's step was 1 iff its skip counter was < 64
-        const bool dup = lane > 0 && ((sk - 1) >> 5) == 1;
-        const bool conflict = window_conflict<kWin>(h, a, dup);  // VALU under the table read
-        const bool hit = be32_at(inw, cand) == cur;  // found_match :259-265
-        const uint64_t stop = __ballot(!valid || conflict || hit);
-        const uint32_t f = (uint32_t)__builtin_ctzll(stop);  // < kWin + 1
-        // lanes before f are exact misses: update_hash_table :303-307
-        if (lane < f) table[a] = (uint16_t)(pk - 1);
-        if (lane < f) table[h] = (uint16_t)pk;
-        const uint64_t match = __ballot(valid && !conflict && hit);
-        if ((match >> f) & 1) {
-            const uint32_t pf = __builtin_amdgcn_readlane(pk, f);
-            const uint32_t cf = __builtin_amdgcn_readlane(cand, f);
-            const uint32_t hf = __builtin_amdgcn_readlane(h, f);
-            if (pf > lit) o = emit_literal(ob, o, inb, lit, pf - lit, lane);
-            uint32_t len = 4;  // find_copy_length :61-72, limit = block end
-            for (;;) {
-                const uint32_t qq = pf + len + lane;
-                const bool ok = qq < L && inb[qq] == inb[cf + len + lane];
-                const uint64_t bad = __ballot(!ok);
-                if (bad) { len += (uint32_t)__builtin_ctzll(bad); break; }
-                len += 64;
-            }
-            o = emit_copy(ob, o, len, pf - cf, lane);
-            if (lane == 0) table[hf] = (uint16_t)pf;  // emit_copy :328
-            skip = 32;
-            p = pf + len;
-            lit = p;
-        } else {
-            // f misses consumed; f stops at a conflict (retried exactly as the
-            // next window's lane 0) or at the block end
-            p = p + skipsum(skip + f) - skipsum(skip);
-            skip += f;
-        }
-    }
-    if (L > lit) o = emit_literal(ob, o, inb, lit, L - lit, lane);  // exhaust_input + emit_literal
-    if (lane == 0) sizes[u] = o;
 }
 
 // ---------------------------------------------------------------------------
@@ -1420,32 +1181,6 @@ __global__ __launch_bounds__(1024) void k3_scan(const uint32_t *__restrict__ siz
 }
 
 // ---------------------------------------------------------------------------
-// K3b: gather each unit's bytes from its 16-aligned scratch slot to its
-// (byte-aligned) place in the output.  Destination writes are dword-aligned;
-// the source side is realigned with v_alignbyte.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k3_gather(const uint8_t *__restrict__ scratch, uint64_t stride,
-                                                 const uint32_t *__restrict__ sizes,
-                                                 const uint64_t *__restrict__ offsets, uint8_t *__restrict__ out)
-{
-    const uint32_t u = blockIdx.x;
-    const uint32_t t = threadIdx.x;
-    const uint8_t *src = scratch + (uint64_t)u * stride;
-    const uint32_t *srcw = reinterpret_cast<const uint32_t *>(src);
-    uint8_t *dst = out + offsets[u];
-    const uint32_t len = sizes[u];
-    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 3);
-    uint32_t head = (4 - mis) & 3;
-    if (head > len) head = len;
-    if (t < head) dst[t] = src[t];
-    const uint32_t nw = (len - head) >> 2;
-    uint32_t *dstw = reinterpret_cast<uint32_t *>(dst + head);
-    for (uint32_t k = t; k < nw; k += 256) dstw[k] = le32_at(srcw, head + 4 * k);
-    const uint32_t tail0 = head + 4 * nw;
-    if (t < len - tail0) dst[tail0 + t] = src[tail0 + t];
-}
-
-// ---------------------------------------------------------------------------
 // K4: one wave per unit.  The compressed unit streams through a 512-byte
 // register window (cur = bytes [B, B+256), nxt = [B+256, B+512), one dword
 // per lane, nxt prefetched a window ahead).  Each batch parses the elements
@@ -1583,7 +1318,7 @@ __device__ uint64_t g_k4_stats[32768 * 8];
 template <bool BACK>
 __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets,
                                         uint64_t n, uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
-                                        uint32_t ring, uint32_t allow_back, uint8_t *__restrict__ out,
+                                        uint32_t ring, uint32_t allow_back, uint32_t bias, uint8_t *__restrict__ out,
                                         int32_t *__restrict__ status, uint32_t u)
 {
     // copy source positions: relative to the unit start, negative = an earlier unit (pass 2 only)
@@ -1593,7 +1328,8 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     const uint32_t M = ring - 1;
     const uint32_t lane = threadIdx.x;
     const uint64_t ix0 = offsets[u], ix1 = offsets[u + 1];
-    const uint64_t c0 = ix0 & kIdxOffMask, c1n = ix1 & kIdxOffMask;
+    // comp is 4-byte aligned; the stream starts `bias` bytes into it
+    const uint64_t c0 = (ix0 & kIdxOffMask) + bias, c1n = (ix1 & kIdxOffMask) + bias;
     const uint32_t skip0 = (uint32_t)(ix0 >> kIdxSkipShift), skip1 = (uint32_t)(ix1 >> kIdxSkipShift);
     const uint64_t base = (uint64_t)u * unit;
     const uint32_t want = (uint32_t)((n - base) < unit ? (n - base) : unit);
@@ -1601,7 +1337,7 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     // the unit's compressed bytes: up to the next entry, or (its last element
     // straddling out) as far as the stream goes
     uint64_t c1 = c1n;
-    if (skip1) c1 = offsets[(n + unit - 1) / unit] & kIdxOffMask;
+    if (skip1) c1 = (offsets[(n + unit - 1) / unit] & kIdxOffMask) + bias;
     if (c1 > c0 + 0x7FFFFFFFull) c1 = c0 + 0x7FFFFFFFull;
     if (c1 < c0 || ((skip0 | skip1) && !allow_back)) st = SNAPPY_ST_TRUNCATED;
     const uint32_t clen = st == SNAPPY_ST_OK ? (uint32_t)(c1 - c0) : 0u;
@@ -2009,16 +1745,16 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_decompress_units(
     const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets, uint64_t n, uint32_t unit,
-    uint32_t hdr_mode, uint64_t header_value, uint32_t ring, uint32_t allow_back, uint8_t *__restrict__ out,
+    uint32_t hdr_mode, uint64_t header_value, uint32_t ring, uint32_t allow_back, uint32_t bias, uint8_t *__restrict__ out,
     int32_t *__restrict__ status)
 {
-    k4_body<false>(comp, offsets, n, unit, hdr_mode, header_value, ring, allow_back, out, status, blockIdx.x);
+    k4_body<false>(comp, offsets, n, unit, hdr_mode, header_value, ring, allow_back, bias, out, status, blockIdx.x);
 }
 
 __global__ __launch_bounds__(64) void k4_decompress_back(const uint8_t *__restrict__ comp,
                                                          const uint64_t *__restrict__ offsets, uint64_t n,
                                                          uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
-                                                         uint32_t ring, uint8_t *__restrict__ out,
+                                                         uint32_t ring, uint32_t bias, uint8_t *__restrict__ out,
                                                          int32_t *__restrict__ status)
 {
     // status[units + 1] == 0: pass 1 deferred nothing (the common case: every wave leaves at once)
@@ -2028,7 +1764,7 @@ __global__ __launch_bounds__(64) void k4_decompress_back(const uint8_t *__restri
     if (threadIdx.x == 0) tk = atomicAdd(reinterpret_cast<uint32_t *>(status + gridDim.x), 1u);
     const uint32_t u = __builtin_amdgcn_readfirstlane(tk);
     if (status[u] != SNAPPY_ST_DEFER) return;
-    k4_body<true>(comp, offsets, n, unit, hdr_mode, header_value, ring, 1u, out, status, u);
+    k4_body<true>(comp, offsets, n, unit, hdr_mode, header_value, ring, 1u, bias, out, status, u);
 }
 // ---------------------------------------------------------------------------
 // K5: block index of a SINGLE-layout stream (one wave).  The stream is

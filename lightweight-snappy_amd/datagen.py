@@ -26,9 +26,21 @@ def lib():
     return _lib
 
 
+GEN_CHUNK = 1 << 20  # the generators are counter-based per 1 MiB (csrc/datagen.c)
+
+
 def fill(out: np.ndarray, kind: str, seed: int, offset: int = 0, threads: int = 8) -> np.ndarray:
     """Fill a contiguous uint8 array with bytes [offset, offset+len) of a generator."""
     assert out.dtype == np.uint8 and out.flags["C_CONTIGUOUS"]
+    lead = offset % GEN_CHUNK
+    if lead and kind != "L" and out.size:  # unaligned start: the first chunk through a bounce buffer
+        head = min(out.size, GEN_CHUNK - lead)
+        tmp = np.empty(lead + head, dtype=np.uint8)
+        fill(tmp, kind, seed, offset - lead, threads)
+        out[:head] = tmp[lead:]
+        if head < out.size:
+            fill(out[head:], kind, seed, offset + head, threads)
+        return out
     rc = lib().snappy_gen_fill_at(out.ctypes.data_as(ctypes.c_void_p), out.size, offset, ord(kind), seed, threads)
     if rc != 0:
         raise ValueError(f"datagen kind={kind!r} offset={offset}: rc={rc}")

@@ -1,7 +1,8 @@
-"""CPU, world_size 2 over gloo: the sharded SINGLE-layout stream assembled
-by dist.assemble is byte-identical to the whole-stream reference output (the
-per-shard codec here is the oracle: the GPU path is exercised by bench.py's
-multi-GPU run and by the gpu tests of the same shard flags)."""
+"""World size 2-3 over gloo.  CPU: the sharded SINGLE-layout stream assembled
+by dist.assemble is byte-identical to the whole-stream reference output with
+the oracle as the per-shard codec.  GPU (ranks sharing cuda:0): the same
+with the HIP shard path, and bench.py's own rank spawning, C2/C3 exchange
+and strong-scaling pieces."""
 import ctypes
 import os
 import socket
@@ -93,3 +94,97 @@ def test_shard_range_covers():
                 assert off % BLOCK == 0
                 pos = off + ln if ln else pos
             assert sum(ln for _, ln in spans) == n
+
+
+def _gpu_worker(rank, world, port, n, layout, chunk, q):
+    """One rank of the HIP shard path: ranks share cuda:0, collectives over gloo."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import dist as sdist
+        import snappy_amd
+        torch.cuda.set_device(0)
+        codec = snappy_amd.Codec(0)
+        a = datagen.make("T", n, 78)
+        unit = BLOCK if layout == snappy_amd.SINGLE else chunk
+        off, ln = sdist.shard_range(n, world, rank, unit)
+        x = torch.from_numpy(a[off:off + ln].copy()).cuda()
+        flags = snappy_amd.NO_PREAMBLE if (layout == snappy_amd.SINGLE and off > 0) else 0
+        hv = n if layout == snappy_amd.SINGLE else ln
+        units = codec.num_units(ln, chunk, layout)
+        out = torch.empty(max(codec.max_output(ln, chunk, layout), 16), dtype=torch.uint8, device="cuda")
+        offs = torch.empty(units + 1, dtype=torch.int64, device="cuda")
+        clen = codec.compress_ptr_ex(x.data_ptr(), ln, chunk, layout, flags, hv, out.data_ptr(), offs.data_ptr())
+        # C2 over gloo: the whole stream and its global index on every rank
+        stream, index = sdist.assemble(out[:clen].cpu(), offs.cpu())
+        # each rank decodes its own blocks from the assembled stream (shard of the global index)
+        u0 = off // unit
+        mine = index[u0:u0 + units + 1].cuda() - int(index[u0])
+        sub = stream[int(index[u0]):int(index[u0 + units])].cuda()
+        back = torch.empty(max(ln, 1), dtype=torch.uint8, device="cuda")
+        codec.decompress_ptr_ex(sub.data_ptr(), mine.data_ptr(), ln, chunk, layout, flags, hv, back.data_ptr())
+        ok_dec = bool(torch.equal(back[:ln], x))
+        if layout == snappy_amd.SINGLE:
+            want = oracle.compress(a.tobytes())
+        else:
+            want = oracle.compress_streams(a, chunk)[0].tobytes()
+        q.put((rank, stream.numpy().tobytes() == want, ok_dec, len(index)))
+        codec.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n,layout,chunk", [(2, 300 * BLOCK + 4567, 0, BLOCK), (2, 9 << 20, 1, 32768),
+                                                  (3, 50 * BLOCK, 0, BLOCK)])
+def test_gpu_sharded_stream_identical(world, n, layout, chunk):
+    """The HIP shard path (snappy_amd_compress_device_ex with NO_PREAMBLE on
+    ranks > 0), world 2-3 on one GPU: the assembled stream is byte-identical
+    to the 1-rank stream (== the reference's), and every rank decodes its
+    blocks from it."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, n, layout, chunk, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(60)
+    assert all(same and dec for _, same, dec, _ in res), res
+
+
+def _bench(*args):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, "\n".join(l for l in r.stderr.splitlines() if l.startswith("[rank"))[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+def test_bench_spawns_ranks_weak():
+    """bench.py --gpus 2 (no launcher): spawns two ranks (gloo rehearsal on one
+    GPU), prints one line with n_gpus 2, C2/C3 timed and verified."""
+    d = _bench("--gpus", "2", "--dist-backend", "gloo", "--bytes-per-gpu", str(64 << 20), "--steps", "2",
+               "--warmup", "1", "--no-host-e2e")
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["round_trip_ok"]
+    assert d["exchange"]["verified"] and d["exchange"]["c2_stream_allgather"]["ms"] > 0
+    assert d["config"]["total_bytes"] == 2 * (64 << 20)
+
+
+@pytest.mark.gpu
+def test_bench_strong_pieces():
+    """--total-bytes fixes the job (strong scaling); --piece-bytes splits a
+    rank's range into several compress calls, SINGLE layout (one stream)."""
+    d = _bench("--gpus", "2", "--dist-backend", "gloo", "--workload", "text64k", "--total-bytes",
+               str(100 * BLOCK * 2 + 12345), "--piece-bytes", str(40 * BLOCK), "--steps", "2", "--warmup", "1",
+               "--no-host-e2e")
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["round_trip_ok"]
+    assert d["config"]["pieces_per_gpu"] == 3 and d["exchange"]["verified"]

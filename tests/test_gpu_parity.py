@@ -373,3 +373,55 @@ def test_foreign_streams_large(codec):
         n, offs = codec.index_tensor(d)
         back = codec.decompress_tensor(d, offs, n, layout=snappy_amd.SINGLE)
         assert back.cpu().numpy().tobytes() == want, seed
+
+
+def test_decode10g_full_size(codec):
+    """BASELINE configs[4] at full size: one SINGLE stream of >= 10 GB
+    (18.5 GB of text, 282,000+ blocks, compressed in 8 GiB pieces as bench.py
+    does), decoded in one K4 launch with a global block index whose
+    compressed offsets pass 2^32.  Sampled blocks (both ends, around the 2^32
+    compressed offset and the 2^32 output offset) are bit-exact against the
+    oracle's compress_next_block; the whole decode equals the input."""
+    import ctypes
+
+    import torch
+    GiB, B = 1 << 30, 65536
+    n = (18_500_000_000 // B) * B
+    base = torch.from_numpy(datagen.make("T", GiB, 4321)).cuda()
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    for o in range(0, n, GiB):  # the text GiB tiled (decoder input variety is per block)
+        m = min(GiB, n - o)
+        x[o:o + m] = base[:m]
+    del base
+    piece = 8 * GiB
+    out = torch.empty(sum(codec.max_output(min(piece, n - o), B, snappy_amd.SINGLE) for o in range(0, n, piece)),
+                      dtype=torch.uint8, device="cuda")
+    codec._bind_stream()
+    idx, pos = [], 0
+    for o in range(0, n, piece):
+        m = min(piece, n - o)
+        offs = torch.empty(m // B + 2, dtype=torch.int64, device="cuda")
+        clen = codec.compress_ptr_ex(x.data_ptr() + o, m, B, snappy_amd.SINGLE, snappy_amd.NO_PREAMBLE if o else 0,
+                                     n, out.data_ptr() + pos, offs.data_ptr())
+        idx.append(offs[:(m + B - 1) // B] + pos)
+        pos += clen
+    idx = torch.cat(idx + [torch.tensor([pos], dtype=torch.int64, device="cuda")])
+    assert pos >= 10_000_000_000 and idx.numel() == n // B + 1
+    back = torch.empty(n, dtype=torch.uint8, device="cuda")
+    codec.decompress_ptr(out.data_ptr(), idx.data_ptr(), n, B, snappy_amd.SINGLE, back.data_ptr())
+    assert torch.equal(back, x)
+    del back
+    # sampled blocks against the oracle
+    hidx = idx.cpu().numpy()
+    u32 = int(np.searchsorted(hidx, 1 << 32)) - 1  # the block whose compressed bytes cross 2^32
+    o32 = (1 << 32) // B
+    units = n // B
+    tmp = np.empty(B + B // 32 + 64, dtype=np.uint8)
+    hdr = snappy_amd.varint_encode(n)
+    for u in sorted({0, 1, 2, u32 - 1, u32, u32 + 1, o32 - 1, o32, o32 + 1, units - 2, units - 1}):
+        blk = x[u * B:(u + 1) * B].cpu().numpy()
+        m = oracle.orc().oracle_compress_block(blk.ctypes.data_as(ctypes.c_void_p), blk.size,
+                                               tmp.ctypes.data_as(ctypes.c_void_p))
+        want = (hdr if u == 0 else b"") + tmp[:m].tobytes()
+        got = out[int(hidx[u]):int(hidx[u + 1])].cpu().numpy().tobytes()
+        assert got == want, u

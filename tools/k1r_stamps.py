@@ -14,8 +14,8 @@ c = snappy_amd.Codec(0)
 comp, offs = c.compress_tensor(x, chunk=chunk, layout=snappy_amd.STREAMS)
 torch.cuda.synchronize()
 class Ctx(ctypes.Structure):
-    _fields_ = [("device", ctypes.c_int), ("own", ctypes.c_void_p), ("stream", ctypes.c_void_p), ("scratch", ctypes.c_void_p),
-                ("scratch_cap", ctypes.c_size_t), ("sizes", ctypes.c_void_p), ("sizes_cap", ctypes.c_size_t),
+    _fields_ = [("device", ctypes.c_int), ("own", ctypes.c_void_p), ("stream", ctypes.c_void_p),
+                ("sizes", ctypes.c_void_p), ("sizes_cap", ctypes.c_size_t),
                 ("tokens", ctypes.c_void_p), ("tokens_cap", ctypes.c_size_t)]
 ctx = ctypes.cast(c._h, ctypes.POINTER(Ctx)).contents
 units = n // chunk

@@ -18,8 +18,8 @@ torch.cuda.synchronize()
 lib = snappy_amd.lib()
 # the context's token buffer pointer is private: re-run through a probe kernel is overkill; read via hipMemcpy of ctx->tokens
 class Ctx(ctypes.Structure):
-    _fields_ = [("device", ctypes.c_int), ("own", ctypes.c_void_p), ("stream", ctypes.c_void_p), ("scratch", ctypes.c_void_p),
-                ("scratch_cap", ctypes.c_size_t), ("sizes", ctypes.c_void_p), ("sizes_cap", ctypes.c_size_t),
+    _fields_ = [("device", ctypes.c_int), ("own", ctypes.c_void_p), ("stream", ctypes.c_void_p),
+                ("sizes", ctypes.c_void_p), ("sizes_cap", ctypes.c_size_t),
                 ("tokens", ctypes.c_void_p), ("tokens_cap", ctypes.c_size_t)]
 ctx = ctypes.cast(c._h, ctypes.POINTER(Ctx)).contents
 units = n // chunk

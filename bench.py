@@ -81,9 +81,13 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL, the real path) or gloo (CPU collectives; rehearsal with ranks sharing a GPU)")
     ap.add_argument("--cpu-sample-bytes", type=int, default=GiB)
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
-                    help="rocprofv3 PMC summary giving HBM traffic per launch (tools/pmc_summary.py)")
-    return ap.parse_args()
+    ap.add_argument("--pmc", default=None,
+                    help="rocprofv3 PMC summary giving HBM traffic per launch (default profiles/pmc_<workload>.json, "
+                         "written by tools/pmc_summary.py)")
+    a = ap.parse_args()
+    if a.pmc is None:
+        a.pmc = os.path.join(ROOT, "profiles", f"pmc_{a.workload}.json")
+    return a
 
 
 def spawn_ranks(n: int) -> int:
@@ -98,12 +102,19 @@ def spawn_ranks(n: int) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
-def cpu_share() -> int:
-    """Host cores this process may run on (the box's lease share, not the machine)."""
+def cpu_share() -> tuple:
+    """(threads to use, note): the GPU box's CPU share for one GPU is what its
+    environment sets OMP_NUM_THREADS to (16); the affinity mask and
+    os.cpu_count() show the whole machine, which other jobs share."""
     try:
-        return len(os.sched_getaffinity(0))
+        visible = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
-        return os.cpu_count() or 1
+        visible = os.cpu_count() or 1
+    lease = os.environ.get("OMP_NUM_THREADS")
+    if lease and lease.isdigit() and 0 < int(lease) <= visible:
+        return int(lease), (f"{lease} threads = this GPU's CPU share on the box (OMP_NUM_THREADS); "
+                            f"the machine shows {visible} CPUs, shared with the other GPUs' jobs")
+    return visible, f"every CPU in this process's affinity mask ({visible})"
 
 
 def cpu_model() -> str:
@@ -142,7 +153,7 @@ def cpu_baseline(kind: str, seed: int, chunk: int, layout: int, sample: int, dec
                       f" + decompress {a.size / (t2 - t1) / 1e6:.1f} MB/s, oracle/snappy_oracle.c -O2, 1 thread,"
                       f" {cpu_model()}"}
     # every host core this process may use, over independent units
-    threads = cpu_share()
+    threads, note = cpu_share()
     t0 = time.perf_counter()
     if layout == snappy_amd.STREAMS:
         payload, offs = oracle.compress_streams(a, chunk, threads=threads)
@@ -156,8 +167,7 @@ def cpu_baseline(kind: str, seed: int, chunk: int, layout: int, sample: int, dec
     assert np.array_equal(back, a)
     allc = {"value": round(a.size / ((t2 - t1) if decode_only else (t2 - t0)) / 1e6, 2), "unit": "MB/s",
             "cores": threads, "kind": "port",
-            "cores_note": f"os.sched_getaffinity: {threads} of the {os.cpu_count()} CPUs the machine shows "
-                          f"(the GPU box's CPU share)",
+            "cores_note": note,
             "compress_MBps": round(a.size / (t1 - t0) / 1e6, 1),
             "decompress_MBps": round(a.size / (t2 - t1) / 1e6, 1)}
     return base, allc

@@ -37,6 +37,7 @@ extern "C" {
 #define SNAPPY_AMD_ERR_IO (-8)         /* FILE* read/write failure                */
 #define SNAPPY_AMD_ERR_UNSUPPORTED (-9)
 #define SNAPPY_AMD_ERR_TIMEOUT (-10)   /* a block waited too long for an earlier one  */
+#define SNAPPY_AMD_ERR_INDEX (-11)     /* a sidecar index that does not fit the stream */
 
 /* Block size of the reference stream format (src/snappy_compression.c:9). */
 #define SNAPPY_AMD_BLOCK 65536u
@@ -53,6 +54,19 @@ int snappy_compress_bst(FILE *file_input, unsigned long long input_size, FILE *f
 /* Status of the last snappy_compress / snappy_decompress call on this
  * thread (the reference signatures cannot return one). */
 int snappy_amd_last_status(void);
+
+/* Sidecar block index (the stream format has no block
+ * markers).  File layout, little-endian u64 words: SNAPPY_AMD_IDX_MAGIC, N
+ * (decoded bytes), count = ceil(N/65536) + 1, then `count` block-index
+ * entries in the format of snappy_amd_decompress_device below (byte offsets
+ * from the start of the stream, its varint preamble included; the last entry
+ * is the stream length).  With it, decoding skips the index pass. */
+#define SNAPPY_AMD_IDX_MAGIC 0x3158444941504e53ull /* "SNPAIDX1" */
+/* snappy_compress() that also writes the sidecar index of its output to idx */
+int snappy_compress_file_indexed(FILE *file_input, unsigned long long input_size, FILE *file_compressed, FILE *idx);
+/* snappy_decompress() using a sidecar index (SNAPPY_AMD_ERR_INDEX if it does
+ * not describe this stream) */
+int snappy_decompress_file_indexed(FILE *file_input, FILE *idx, FILE *file_decompressed);
 
 /* ---- varint preamble (src/varint.c) ---------------------------------- */
 /* LEB128 of n into out (<= 10 bytes); returns bytes written. varint.c:12-20 */

@@ -18,10 +18,14 @@ extern "C" {
 int snappy_amd_host_compress(const uint8_t *in, size_t n, uint64_t header_value, uint8_t *out, size_t cap,
                              size_t *out_len);
 int snappy_amd_host_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len);
+/* the same with a sidecar block index (count entries) instead of the index pass */
+int snappy_amd_host_decompress_idx(const uint8_t *in, size_t n, const uint64_t *idx, size_t count, uint8_t *out,
+                                   size_t cap, size_t *out_len);
 /* Streaming form of snappy_compress(): reads fin from its current position
  * to EOF in 64 MiB chunks, writes the same bytes as the whole-input call
- * (varint(header_value) ++ blocks) to fout; *bytes_in = bytes read. */
-int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, uint64_t *bytes_in);
+ * (varint(header_value) ++ blocks) to fout, and (fidx != NULL) the sidecar
+ * index of snappy_amd.h to fidx; *bytes_in = bytes read. */
+int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, FILE *fidx, uint64_t *bytes_in);
 #ifdef __cplusplus
 }
 #endif

@@ -436,6 +436,7 @@ namespace {
 struct StreamSlot {
     snappy_amd_ctx *c = nullptr;
     uint8_t *h_in = nullptr, *h_out = nullptr;
+    uint64_t *h_idx = nullptr;  // the chunk's block index, for the sidecar file
     uint8_t *d_in = nullptr, *d_out = nullptr;
     uint64_t *d_idx = nullptr;
     size_t n = 0;
@@ -464,30 +465,47 @@ int slot_init(StreamSlot &s, int device)
     const size_t units = kStreamChunk / SNAPPY_AMD_BLOCK;
     if (hipHostMalloc(&s.h_in, kStreamChunk, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&s.h_out, maxo, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&s.h_idx, (units + 1) * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
         hipMalloc(&s.d_in, kStreamChunk) != hipSuccess || hipMalloc(&s.d_out, maxo) != hipSuccess ||
         hipMalloc(&s.d_idx, (units + 1) * sizeof(uint64_t)) != hipSuccess)
         return SNAPPY_AMD_ERR_DEVICE;
     return SNAPPY_AMD_OK;
 }
 
-// finish slot s: its compressed size is in s.c->h_total once its stream drains
-int slot_drain(StreamSlot &s, FILE *fout)
+// finish slot s: its compressed size is in s.c->h_total once its stream drains.
+// With a sidecar file, the chunk's block index goes out too, shifted by the
+// stream bytes written before it (*base); the stream-end entry is left to the caller.
+int slot_drain(StreamSlot &s, FILE *fout, FILE *fidx, uint64_t *base)
 {
     if (!s.busy) return SNAPPY_AMD_OK;
     s.busy = false;
     HIP_OK(hipStreamSynchronize(s.c->stream));
     const size_t len = (size_t)*s.c->h_total;
+    const size_t units = (s.n + SNAPPY_AMD_BLOCK - 1) / SNAPPY_AMD_BLOCK;
     HIP_OK(hipMemcpyAsync(s.h_out, s.d_out, len, hipMemcpyDeviceToHost, s.c->stream));
+    if (fidx) HIP_OK(hipMemcpyAsync(s.h_idx, s.d_idx, units * sizeof(uint64_t), hipMemcpyDeviceToHost, s.c->stream));
     HIP_OK(hipStreamSynchronize(s.c->stream));
     if (len && fwrite(s.h_out, 1, len, fout) != len) return SNAPPY_AMD_ERR_IO;
+    if (fidx) {
+        for (size_t i = 0; i < units; i++) s.h_idx[i] += *base;
+        if (fwrite(s.h_idx, sizeof(uint64_t), units, fidx) != units) return SNAPPY_AMD_ERR_IO;
+    }
+    *base += len;
     return SNAPPY_AMD_OK;
 }
 }  // namespace
 
-int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, uint64_t *bytes_in)
+int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, FILE *fidx, uint64_t *bytes_in)
 {
     std::lock_guard<std::mutex> lk(g_mu);
     if (!fin || !fout) return SNAPPY_AMD_ERR_ARG;
+    uint64_t base = 0;  // stream bytes written so far
+    long idx_hdr = -1;
+    if (fidx) {  // sidecar header; N and the entry count are patched at the end
+        idx_hdr = ftell(fidx);
+        const uint64_t h[3] = {SNAPPY_AMD_IDX_MAGIC, header_value, 0};
+        if (idx_hdr < 0 || fwrite(h, sizeof(uint64_t), 3, fidx) != 3) return SNAPPY_AMD_ERR_IO;
+    }
     int dev = 0;
     if (const char *e = getenv("SNAPPY_AMD_DEVICE")) dev = atoi(e);
     int rc;
@@ -515,17 +533,35 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
         s.busy = true;
         // chunk k-1 out while chunk k runs, then chunk k+1 in (its slot is free
         // once chunk k-1 drained)
-        if ((rc = slot_drain(o, fout))) return rc;
+        if ((rc = slot_drain(o, fout, fidx, &base))) return rc;
         n = read_full(fin, o.h_in, kStreamChunk);
         if (ferror(fin)) return SNAPPY_AMD_ERR_IO;
     }
-    for (auto &s : g_slots)
-        if ((rc = slot_drain(s, fout))) return rc;
+    // the slots drain in chunk order: the one holding the last chunk goes last
+    const uint32_t last = total_in ? (uint32_t)(((total_in + kStreamChunk - 1) / kStreamChunk - 1) & 1) : 0;
+    if ((rc = slot_drain(g_slots[last ^ 1], fout, fidx, &base))) return rc;
+    if ((rc = slot_drain(g_slots[last], fout, fidx, &base))) return rc;
+    if (fidx) {
+        const uint64_t units = (total_in + SNAPPY_AMD_BLOCK - 1) / SNAPPY_AMD_BLOCK;
+        const uint64_t cnt = total_in ? units + 1 : 0;
+        if (total_in && fwrite(&base, sizeof(uint64_t), 1, fidx) != 1) return SNAPPY_AMD_ERR_IO;
+        // an index describes the blocks actually written: N = the bytes read
+        const uint64_t h[2] = {total_in, cnt};
+        if (fseek(fidx, idx_hdr + 8, SEEK_SET) || fwrite(h, sizeof(uint64_t), 2, fidx) != 2 ||
+            fseek(fidx, 0, SEEK_END))
+            return SNAPPY_AMD_ERR_IO;
+    }
     if (bytes_in) *bytes_in = total_in;
     return SNAPPY_AMD_OK;
 }
 
 int snappy_amd_host_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len)
+{
+    return snappy_amd_host_decompress_idx(in, n, nullptr, 0, out, cap, out_len);
+}
+
+int snappy_amd_host_decompress_idx(const uint8_t *in, size_t n, const uint64_t *idx, size_t count, uint8_t *out,
+                                   size_t cap, size_t *out_len)
 {
     std::lock_guard<std::mutex> lk(g_mu);
     if (!out_len || (!in && n)) return SNAPPY_AMD_ERR_ARG;
@@ -543,9 +579,15 @@ int snappy_amd_host_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t
     if ((rc = grow(reinterpret_cast<void **>(&c->d_b), &c->d_b_cap, N + 16))) return rc;
     if ((rc = grow(reinterpret_cast<void **>(&c->d_idx), &c->d_idx_cap, (units + 2) * sizeof(uint64_t)))) return rc;
     HIP_OK(hipMemcpyAsync(c->d_a, in, n, hipMemcpyHostToDevice, c->stream));
-    size_t got = 0;
-    rc = snappy_amd_index_device(c, c->d_a, n, c->d_idx, units + 1, &got);
-    if (rc) return rc;
+    if (idx) {  // a sidecar index: no index pass; it must describe this stream
+        if (count != units + 1 || (idx[units] & ((1ull << SNAPPY_AMD_IDX_OFFSET_BITS) - 1)) != n)
+            return SNAPPY_AMD_ERR_INDEX;
+        HIP_OK(hipMemcpyAsync(c->d_idx, idx, count * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    } else {
+        size_t got = 0;
+        rc = snappy_amd_index_device(c, c->d_a, n, c->d_idx, units + 1, &got);
+        if (rc) return rc;
+    }
     if (N == 0) { *out_len = 0; return SNAPPY_AMD_OK; }
     rc = snappy_amd_decompress_device(c, c->d_a, c->d_idx, (size_t)N, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE, c->d_b);
     if (rc) return rc;

@@ -98,30 +98,70 @@ void snappy_compress(FILE *file_input, unsigned long long input_size, FILE *file
     /* header = the caller's input_size, as the reference writes it; an empty
      * read writes nothing (snappy_compression.c:417-421) */
     int rc = (file_input && file_compressed)
-                 ? snappy_amd_host_compress_file(file_input, (uint64_t)input_size, file_compressed, NULL)
+                 ? snappy_amd_host_compress_file(file_input, (uint64_t)input_size, file_compressed, NULL, NULL)
                  : SNAPPY_AMD_ERR_ARG;
     g_last_status = rc;
     if (rc != SNAPPY_AMD_OK) fprintf(stderr, "snappy_compress: error %d\n", rc);
 }
 
-int snappy_decompress(FILE *file_input, FILE *file_decompressed)
+/* sidecar index file -> its entries (malloc'd) */
+static int read_index(FILE *f, uint64_t **entries, size_t *count)
+{
+    uint64_t h[3];
+    if (fread(h, sizeof(uint64_t), 3, f) != 3 || h[0] != SNAPPY_AMD_IDX_MAGIC) return SNAPPY_AMD_ERR_INDEX;
+    if (h[2] > (h[1] >> 16) + 2) return SNAPPY_AMD_ERR_INDEX;
+    uint64_t *e = (uint64_t *)malloc((h[2] ? h[2] : 1) * sizeof(uint64_t));
+    if (!e) return SNAPPY_AMD_ERR_IO;
+    if (fread(e, sizeof(uint64_t), h[2], f) != h[2]) { free(e); return SNAPPY_AMD_ERR_INDEX; }
+    *entries = e;
+    *count = (size_t)h[2];
+    return SNAPPY_AMD_OK;
+}
+
+static int decompress_file(FILE *file_input, FILE *idx, FILE *file_decompressed, const char *what)
 {
     uint8_t *in = NULL, *out = NULL;
-    size_t n = 0, len = 0;
+    uint64_t *ent = NULL;
+    size_t n = 0, len = 0, count = 0;
     int rc = (file_input && file_decompressed) ? slurp(file_input, &in, &n) : SNAPPY_AMD_ERR_ARG;
+    if (rc == SNAPPY_AMD_OK && idx) rc = read_index(idx, &ent, &count);
     if (rc == SNAPPY_AMD_OK && n > 0) {
         uint64_t N = 0;
         rc = snappy_uncompressed_length(in, n, &N);
         if (rc == SNAPPY_AMD_OK) {
             out = (uint8_t *)malloc(N ? N : 1);
-            rc = out ? snappy_amd_host_decompress(in, n, out, N, &len) : SNAPPY_AMD_ERR_IO;
+            rc = !out ? SNAPPY_AMD_ERR_IO
+                      : idx ? snappy_amd_host_decompress_idx(in, n, ent, count, out, N, &len)
+                            : snappy_amd_host_decompress(in, n, out, N, &len);
         }
         if (rc == SNAPPY_AMD_OK && len && fwrite(out, 1, len, file_decompressed) != len) rc = SNAPPY_AMD_ERR_IO;
     }
     free(in);
     free(out);
+    free(ent);
     g_last_status = rc;
-    if (rc != SNAPPY_AMD_OK) fprintf(stderr, "snappy_decompress: error %d\n", rc);
+    if (rc != SNAPPY_AMD_OK) fprintf(stderr, "%s: error %d\n", what, rc);
+    return rc;
+}
+
+int snappy_decompress(FILE *file_input, FILE *file_decompressed)
+{
+    return decompress_file(file_input, NULL, file_decompressed, "snappy_decompress");
+}
+
+int snappy_decompress_file_indexed(FILE *file_input, FILE *idx, FILE *file_decompressed)
+{
+    if (!idx) return g_last_status = SNAPPY_AMD_ERR_ARG;
+    return decompress_file(file_input, idx, file_decompressed, "snappy_decompress_file_indexed");
+}
+
+int snappy_compress_file_indexed(FILE *file_input, unsigned long long input_size, FILE *file_compressed, FILE *idx)
+{
+    int rc = (file_input && file_compressed && idx)
+                 ? snappy_amd_host_compress_file(file_input, (uint64_t)input_size, file_compressed, idx, NULL)
+                 : SNAPPY_AMD_ERR_ARG;
+    g_last_status = rc;
+    if (rc != SNAPPY_AMD_OK) fprintf(stderr, "snappy_compress_file_indexed: error %d\n", rc);
     return rc;
 }
 

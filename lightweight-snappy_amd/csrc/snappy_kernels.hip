@@ -60,8 +60,11 @@ __device__ __forceinline__ uint32_t skipsum(uint32_t m)
 // K1r: register-resident match finder (one wave per unit).
 //
 //  * The unit lives in VGPRs: register r, lane l holds big-endian dword
-//    64 r + l (128 VGPRs v2..v129 for 32 KiB; 65,536-byte blocks continue in
-//    AGPRs a0..a127 + zero spare a128).  A wave-uniform
+//    64 r + l (128 VGPRs v2..v129 hold 32 KiB).  65,536-byte blocks keep a
+//    ring of their last 128 256-byte segments there instead (segment s in
+//    register s % 128, loaded ahead of the probe window; measured on the text
+//    workload only 1.4 % of candidate checks reach further back, and those read
+//    global memory), so both kernels run 3 waves per SIMD.  A wave-uniform
 //    register index goes through s_set_gpr_idx_on.  Any 64 consecutive dwords
 //    d..d+63 sit in registers R = d / 64 and R + 1: merged by one lane select
 //    they are a rotation of the wanted lanes, undone by one ds_bpermute.
@@ -86,8 +89,8 @@ __device__ __forceinline__ uint32_t skipsum(uint32_t m)
 //    probes at their closed-form positions with explicit conflict stops.
 //  * Output is a token list (pos | len << 16, offset); K2s sizes it, K3 places
 //    every unit, K2 writes the bytes.
-// 12 KiB LDS and <= 168 VGPRs -> 12 units per CU (3 waves per SIMD);
-// 65,536-byte blocks (k1r_match_units64): 1 wave per SIMD.
+// 12 KiB LDS and <= 168 VGPRs -> 12 units per CU (3 waves per SIMD), both
+// kernels.
 // ---------------------------------------------------------------------------
 typedef uint32_t v32 __attribute__((ext_vector_type(32)));
 typedef uint32_t __attribute__((aligned(1))) u32u;
@@ -96,9 +99,8 @@ typedef uint16_t __attribute__((aligned(1))) u16u;
 constexpr uint32_t kTagMul = 0x9E3779B1u;
 constexpr uint32_t kRegs = 128;  // VGPRs holding a 32 KiB unit (64 dwords each), + 1 zero spare
 // Register r (wave-uniform) of the resident unit.  g0..g3 are pinned to
-// v2..v129 by the asm constraints (65,536-byte units continue in a0..a128),
-// so the relative move (s_set_gpr_idx_on, SRC0) is exact whatever else the
-// allocator does; AGPRs are read with v_accvgpr_read.
+// v2..v129 by the asm constraints, so the relative move (s_set_gpr_idx_on,
+// SRC0) is exact whatever else the allocator does.
 #define REG_OF_V(r)                                                                                 \
     ({                                                                                              \
         uint32_t _v;                                                                                \
@@ -108,27 +110,24 @@ constexpr uint32_t kRegs = 128;  // VGPRs holding a 32 KiB unit (64 dwords each)
                        "{v[98:129]}"(g3));                                                          \
         _v;                                                                                         \
     })
-// AGPRs a0..a128 are written once by the prologue's v_accvgpr_write asm
-// (with the registers as clobbers, so the kernel allocates them) and are
-// otherwise invisible to the compiler, which never needs AGPRs here
-#define REG_OF_A(r)                                                                                 \
-    ({                                                                                              \
-        uint32_t _v;                                                                                \
-        asm volatile("s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\tv_accvgpr_read_b32 %0, a0\n\ts_set_gpr_idx_off" \
-                     : "=&v"(_v)                                                                    \
-                     : "s"((uint32_t)(r)));                                                         \
-        _v;                                                                                         \
-    })
+// BIG (65,536-byte blocks): the 128 registers are a ring over the block's
+// 256-byte segments -- segment s lives in register s % 128 while it is one of
+// the last 128 loaded (ring_to in k1r_body); older candidates are read from
+// global memory.  s_set_gpr_idx DST mode writes a ring register in place.
+// g0..g3 are only ever read through asm that names v2..v129, so the write is
+// modelled as a use: tied in/out operands make the allocator copy the 128
+// registers (hundreds of spills).  The kernels are checked to keep g0..g3 in
+// place with no VGPR spills (tests/test_abi.py::test_kernel_register_budget).
+#define REG_SET_V(r, val)                                                                            \
+    asm volatile("s_set_gpr_idx_on %0, gpr_idx(DST)\n\tv_mov_b32 v2, %1\n\ts_set_gpr_idx_off"            \
+                 :: "s"((uint32_t)(r)), "v"(val), "{v[2:33]}"(g0), "{v[34:65]}"(g1), "{v[66:97]}"(g2),      \
+                 "{v[98:129]}"(g3) : "memory")
 #define REG_OF(r)                                                                                   \
     ({                                                                                              \
         const uint32_t _rr = (r);                                                                   \
         uint32_t _rv;                                                                               \
-        if constexpr (BIG) {                                                                        \
-            if (_rr < kRegs) _rv = REG_OF_V(_rr);                                                   \
-            else _rv = REG_OF_A(_rr - kRegs);                                                       \
-        } else {                                                                                    \
-            _rv = REG_OF_V(_rr);                                                                    \
-        }                                                                                           \
+        if constexpr (BIG) _rv = REG_OF_V(_rr & (kRegs - 1));                                       \
+        else _rv = REG_OF_V(_rr);                                                                   \
         _rv;                                                                                        \
     })
 
@@ -141,18 +140,13 @@ constexpr uint32_t kRegs = 128;  // VGPRs holding a 32 KiB unit (64 dwords each)
                  : "=&v"(lo), "=&v"(hi)                                                              \
                  : "s"((uint32_t)(r)), "{v[2:33]}"(g0), "{v[34:65]}"(g1), "{v[66:97]}"(g2),              \
                    "{v[98:129]}"(g3))
-#define REG_PAIR_A(r, lo, hi)                                                                        \
-    asm volatile("s_set_gpr_idx_on %2, gpr_idx(SRC0)\n\tv_accvgpr_read_b32 %0, a0\n\t"                    \
-                 "v_accvgpr_read_b32 %1, a1\n\ts_set_gpr_idx_off"                                      \
-                 : "=&v"(lo), "=&v"(hi)                                                              \
-                 : "s"((uint32_t)(r)))
 #define REG_PAIR(r, lo, hi)                                                                          \
     do {                                                                                             \
         const uint32_t _pr = (r);                                                                    \
-        if constexpr (BIG) {                                                                         \
-            if (_pr + 1 < kRegs) REG_PAIR_V(_pr, lo, hi);                                            \
-            else if (_pr >= kRegs) REG_PAIR_A(_pr - kRegs, lo, hi);                                  \
-            else { lo = REG_OF_V(_pr); hi = REG_OF_A(0); }                                           \
+        if constexpr (BIG) { /* ring registers r, r + 1 (mod 128) */                                 \
+            const uint32_t _pq = _pr & (kRegs - 1);                                                  \
+            if (__builtin_expect(_pq != kRegs - 1, 1)) REG_PAIR_V(_pq, lo, hi);                      \
+            else { lo = REG_OF_V(kRegs - 1); hi = REG_OF_V(0); }                                     \
         } else {                                                                                     \
             REG_PAIR_V(_pr, lo, hi);                                                                 \
         }                                                                                            \
@@ -369,8 +363,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     // unit -> registers, big-endian dwords, zero past the end
     v32 g0, g1, g2, g3;
     const bool aligned = ((reinterpret_cast<uintptr_t>(src) & 3) == 0);
-    auto load_word = [&](uint32_t i) -> uint32_t {
-        const uint32_t b = 4 * (64 * i + lane);
+    // big-endian dword k (per lane) of the unit, zero past its end
+    auto load_dw = [&](uint32_t k) -> uint32_t {
+        const uint32_t b = 4 * k;
         uint32_t w = 0;
         if (b + 4 <= L && aligned) {
             w = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(src + b));
@@ -380,6 +375,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         }
         return __builtin_bswap32(w);
     };
+    auto load_word = [&](uint32_t i) -> uint32_t { return load_dw(64 * i + lane); };
 #pragma unroll
     for (int i = 0; i < (int)kRegs; i++) {
         const uint32_t w = load_word(i);
@@ -388,27 +384,32 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         else if (i < 96) g2[i - 64] = w;
         else g3[i - 96] = w;
     }
-    if constexpr (BIG) {
-#define K1R_AW(k) asm volatile("v_accvgpr_write_b32 a" #k ", %0" ::"v"(load_word(kRegs + (k))) : "a" #k)
-#define K1R_AW8(k) K1R_AW(k##0); K1R_AW(k##1); K1R_AW(k##2); K1R_AW(k##3); K1R_AW(k##4); K1R_AW(k##5); K1R_AW(k##6); K1R_AW(k##7)
-        K1R_AW(0); K1R_AW(1); K1R_AW(2); K1R_AW(3); K1R_AW(4); K1R_AW(5); K1R_AW(6); K1R_AW(7);
-        K1R_AW(8); K1R_AW(9);
-        K1R_AW8(1); K1R_AW(18); K1R_AW(19);
-        K1R_AW8(2); K1R_AW(28); K1R_AW(29);
-        K1R_AW8(3); K1R_AW(38); K1R_AW(39);
-        K1R_AW8(4); K1R_AW(48); K1R_AW(49);
-        K1R_AW8(5); K1R_AW(58); K1R_AW(59);
-        K1R_AW8(6); K1R_AW(68); K1R_AW(69);
-        K1R_AW8(7); K1R_AW(78); K1R_AW(79);
-        K1R_AW8(8); K1R_AW(88); K1R_AW(89);
-        K1R_AW8(9); K1R_AW(98); K1R_AW(99);
-        K1R_AW8(10); K1R_AW(108); K1R_AW(109);
-        K1R_AW8(11); K1R_AW(118); K1R_AW(119);
-        K1R_AW(120); K1R_AW(121); K1R_AW(122); K1R_AW(123); K1R_AW(124); K1R_AW(125); K1R_AW(126); K1R_AW(127);
-        K1R_AW(128);  // spare: load_word(256) is zero for 65,536-byte units
-#undef K1R_AW8
-#undef K1R_AW
-    }
+
+    // BIG: segments [seg_hi - 128, seg_hi) are resident in the ring registers
+    uint32_t seg_hi = kRegs;
+    // make segments < need resident (a long jump reloads at most the last 128)
+    auto ring_to = [&](uint32_t need) {
+        if constexpr (BIG) {
+            if (__builtin_expect(need <= seg_hi, 1)) return;
+            for (uint32_t sg = need - seg_hi > kRegs ? need - kRegs : seg_hi; sg < need; sg++)
+                REG_SET_V(sg & (kRegs - 1), load_word(sg));
+            seg_hi = need;
+        }
+    };
+    // lane i <- big-endian dword dd + i: from the registers, or (BIG, a segment
+    // that left the ring) from global memory
+#define CAND_LANES(dd)                                                                             \
+    ({                                                                                             \
+        const uint32_t _cd = (dd);                                                                 \
+        uint32_t _cv;                                                                              \
+        if constexpr (BIG) {                                                                       \
+            if (__builtin_expect((_cd >> 6) + kRegs >= seg_hi, 1)) _cv = DW_LANES(_cd);             \
+            else _cv = load_dw(_cd + lane);                                                        \
+        } else {                                                                                   \
+            _cv = DW_LANES(_cd);                                                                   \
+        }                                                                                          \
+        _cv;                                                                                       \
+    })
 
     uint32_t T = 256, lg = 8;  // set_htable_size :198-204
     while (T < kTable && T < L) { T <<= 1; lg++; }
@@ -457,6 +458,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #define WINDOW_AT(qq)                                                                              \
     do {                                                                                           \
         q0 = (qq);                                                                                 \
+        ring_to((q0 >> 8) + 2); /* BIG: the window's segments and the next */                      \
         d0 = q0 >> 2;                                                                              \
         dr = d0 & 63;                                                                              \
         {                                                                                          \
@@ -497,7 +499,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             for (;;) {
                 if (pf + len >= L) break;
                 const uint32_t qa = pf + len, qb = cand + len;
-                const uint32_t a0 = DW_LANES(qa >> 2), b0 = DW_LANES(qb >> 2);
+                ring_to((qa >> 8) + 2);
+                const uint32_t a0 = DW_LANES(qa >> 2), b0 = CAND_LANES(qb >> 2);
                 const uint32_t va = funnel_bytes(a0, wave_shl1(a0), perm_sel(qa & 3));
                 const uint32_t vb = funnel_bytes(b0, wave_shl1(b0), perm_sel(qb & 3));
                 const uint32_t yy = lane < 63 ? (va ^ vb) : 0;  // lane 63 lacks its successor
@@ -513,7 +516,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     };
     auto match_len = [&](uint32_t pf, uint32_t cand) -> uint32_t {
         const uint32_t pa = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((pf >> 2) + lane) << 2), (int)dv);
-        const uint32_t ca = DW_LANES(cand >> 2);
+        const uint32_t ca = CAND_LANES(cand >> 2);
         const uint32_t pv = funnel_bytes(pa, wave_shl1(pa), perm_sel(pf & 3));
         const uint32_t cv = funnel_bytes(ca, wave_shl1(ca), perm_sel(cand & 3));
         const uint32_t y = pv ^ cv;
@@ -612,7 +615,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     // compare the 64 bytes at pf (dwords from dv) and c (registers)
                     const uint32_t pa = (uint32_t)__builtin_amdgcn_ds_bpermute(
                         (int)(((pf >> 2) + lane) << 2), (int)dv);
-                    const uint32_t ca = DW_LANES(c >> 2);
+                    const uint32_t ca = CAND_LANES(c >> 2);
                     __builtin_amdgcn_sched_barrier(0);
                     // the inserts known before the verdict: misses p_k - 1, p_k and the
                     // probe at f (miss or match) -- all of [lane0 - 1, f] unless f is the
@@ -761,6 +764,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #undef TBL_WRITE3
 #undef TAG_EQ
 #undef LDS_ORDER
+#undef CAND_LANES
     flush_tokens();
     // the tail literal is pseudo-token nt (src/snappy_compression.c:292-297)
     if (lane == 0) {
@@ -795,9 +799,9 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
     k1r_body<false>(in, n, unit, hdr_mode, header_value, tokens, tok_cap, ntok_out, sizes, seg_off, segs);
 }
 
-// 65,536-byte blocks (the reference's MAX_BLOCK_SIZE): unit in 128 VGPRs +
-// 128 AGPRs, one wave per SIMD
-__global__ __launch_bounds__(64, 1) void k1r_match_units64(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
+// 65,536-byte blocks (the reference's MAX_BLOCK_SIZE): a 32 KiB register
+// ring over the block, three waves per SIMD
+__global__ __launch_bounds__(64, 3) void k1r_match_units64(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
                                                             uint32_t hdr_mode, uint64_t header_value,
                                                             uint2 *__restrict__ tokens, uint32_t tok_cap,
                                                             uint32_t *__restrict__ ntok_out,

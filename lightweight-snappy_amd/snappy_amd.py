@@ -34,6 +34,8 @@ ERR_DEVICE = -7
 ERR_IO = -8
 ERR_UNSUPPORTED = -9
 ERR_TIMEOUT = -10
+ERR_INDEX = -11
+IDX_MAGIC = 0x3158444941504E53  # b"SNPAIDX1" as a little-endian u64
 
 BLOCK = 65536
 SINGLE = 0
@@ -51,6 +53,7 @@ _NAMES = {
     ERR_IO: "I/O error",
     ERR_UNSUPPORTED: "unsupported",
     ERR_TIMEOUT: "block dependency wait timed out",
+    ERR_INDEX: "sidecar index does not fit the stream",
 }
 
 # every function include/*.h declares, with its ctypes signature
@@ -59,6 +62,8 @@ _SIGS = {
     "snappy_compress": (None, [_c.c_void_p, _c.c_ulonglong, _c.c_void_p]),
     "snappy_decompress": (_c.c_int, [_c.c_void_p, _c.c_void_p]),
     "snappy_compress_bst": (_c.c_int, [_c.c_void_p, _c.c_ulonglong, _c.c_void_p]),
+    "snappy_compress_file_indexed": (_c.c_int, [_c.c_void_p, _c.c_ulonglong, _c.c_void_p, _c.c_void_p]),
+    "snappy_decompress_file_indexed": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p]),
     "snappy_amd_last_status": (_c.c_int, []),
     "snappy_varint_encode": (_c.c_uint32, [_c.c_uint64, _c.c_void_p]),
     "snappy_varint_decode": (_c.c_uint32, [_c.c_void_p, _c.c_size_t, _c.POINTER(_c.c_uint64)]),
@@ -94,8 +99,11 @@ _SIGS = {
                                             _c.POINTER(_c.c_size_t)]),
     "snappy_amd_host_decompress": (_c.c_int, [_c.c_void_p, _c.c_size_t, _c.c_void_p, _c.c_size_t,
                                               _c.POINTER(_c.c_size_t)]),
-    # FILE* in, header value, FILE* out, bytes read (C stdio streams; used by the C host layer)
-    "snappy_amd_host_compress_file": (_c.c_int, [_c.c_void_p, _c.c_uint64, _c.c_void_p, _c.POINTER(_c.c_uint64)]),
+    "snappy_amd_host_decompress_idx": (_c.c_int, [_c.c_void_p, _c.c_size_t, _c.c_void_p, _c.c_size_t, _c.c_void_p,
+                                                  _c.c_size_t, _c.POINTER(_c.c_size_t)]),
+    # FILE* in, header value, FILE* out, FILE* sidecar (or NULL), bytes read (C stdio streams; the C host layer)
+    "snappy_amd_host_compress_file": (_c.c_int, [_c.c_void_p, _c.c_uint64, _c.c_void_p, _c.c_void_p,
+                                                 _c.POINTER(_c.c_uint64)]),
     # reference Buffer cursor helpers (Buffer* is a struct of two pointers and a u32)
     "init_Buffer": (None, [_c.c_void_p, _c.c_uint]),
     "move_current": (None, [_c.c_void_p, _c.c_uint]),
@@ -190,6 +198,29 @@ def decompress(data) -> bytes:
     out = ctypes.create_string_buffer(max(N, 1))
     got = ctypes.c_size_t(0)
     _check(lib().snappy_decompress_buffer(p, n, out, N, ctypes.byref(got)), "decompress")
+    return out.raw[: got.value]
+
+
+def read_index(data: bytes):
+    """Sidecar index file (snappy_amd.h) -> (N, [entries])."""
+    import struct
+    magic, n, count = struct.unpack_from("<QQQ", data, 0)
+    if magic != IDX_MAGIC or len(data) != 24 + 8 * count:
+        raise SnappyError(ERR_INDEX, "read_index")
+    return n, list(struct.unpack_from(f"<{count}Q", data, 24))
+
+
+def decompress_indexed(data, index_file: bytes) -> bytes:
+    """decompress() with a sidecar index instead of the GPU index pass."""
+    p, n, keep = _buf(data)
+    if n == 0:
+        return b""
+    _, ent = read_index(index_file)
+    arr = (ctypes.c_uint64 * max(len(ent), 1))(*ent)
+    N = uncompressed_length(data)
+    out = ctypes.create_string_buffer(max(N, 1))
+    got = ctypes.c_size_t(0)
+    _check(lib().snappy_amd_host_decompress_idx(p, n, arr, len(ent), out, N, ctypes.byref(got)), "decompress_indexed")
     return out.raw[: got.value]
 
 

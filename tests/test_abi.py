@@ -104,3 +104,38 @@ def test_buffer_cursor_helpers():
     lib.reset(ctypes.byref(b))
     assert b.current == b.beginning and b.bytes_left == 70  # reset leaves bytes_left alone
     ctypes.CDLL(None).free(ctypes.c_void_p(b.beginning))
+
+
+def test_kernel_register_budget(tmp_path):
+    """The gfx950 code object of the built library: the K1r kernels keep the
+    unit in v2..v129 untouched between their register-indexed accesses (the
+    65,536-byte kernel writes its ring only through gpr_idx DST moves), fit
+    3 waves per SIMD (<= 168 VGPRs) and spill nothing (tools/check_ring.py)."""
+    import re
+    import shutil
+    import subprocess
+    import sys
+    llvm = "/opt/rocm/lib/llvm/bin"
+    obj = os.path.join(ROOT, "lightweight-snappy_amd", "build", "snappy_kernels.o")
+    if not (os.path.exists(obj) and os.path.exists(f"{llvm}/llvm-objdump") and shutil.which("objcopy")):
+        pytest.skip("needs the in-tree build object and the ROCm LLVM tools")
+    fat, co = tmp_path / "fat.bin", tmp_path / "k.co"
+    subprocess.run(["objcopy", f"--dump-section=.hip_fatbin={fat}", obj], check=True)
+    subprocess.run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+    notes = subprocess.run([f"{llvm}/llvm-readobj", "--notes", str(co)], check=True, capture_output=True,
+                           text=True).stdout
+    found = 0
+    for blk in notes.split("- .agpr_count")[1:]:
+        name = re.search(r"\.name:\s+(\S+)", blk).group(1)
+        if "k1r_match_units" not in name:
+            continue
+        found += 1
+        vg = int(re.search(r"\.vgpr_count:\s+(\d+)", blk).group(1))
+        sp = int(re.search(r"\.vgpr_spill_count:\s+(\d+)", blk).group(1))
+        assert vg <= 168 and sp == 0, (name, vg, sp)
+    assert found == 2
+    dis = subprocess.run([f"{llvm}/llvm-objdump", "-d", str(co)], check=True, capture_output=True, text=True).stdout
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import check_ring
+    assert check_ring.check(dis) == []

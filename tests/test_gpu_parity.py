@@ -425,3 +425,52 @@ def test_decode10g_full_size(codec):
         want = (hdr if u == 0 else b"") + tmp[:m].tobytes()
         got = out[int(hidx[u]):int(hidx[u + 1])].cpu().numpy().tobytes()
         assert got == want, u
+
+
+def _index_file(n, entries):
+    import struct
+    return struct.pack("<QQQ", snappy_amd.IDX_MAGIC, n, len(entries)) + struct.pack(f"<{len(entries)}Q", *entries)
+
+
+def test_cli_sidecar_index():
+    """`snappy -c -i` writes <out>.idx next to the stream (the
+    streaming compressor's per-chunk indexes, shifted; 150 MiB = 3 pipeline
+    chunks); it equals the index the GPU index pass builds, and `snappy -d -i`
+    decodes with it.  An index of another stream is refused."""
+    import torch
+    exe = os.path.join(ROOT, "lightweight-snappy_amd", "snappy")
+    data = np.concatenate([datagen.make("T", 90 << 20, 51), datagen.make("R", 40 << 20, 52),
+                           datagen.make("T", (20 << 20) + 777, 53)]).tobytes()
+    with tempfile.TemporaryDirectory() as d:
+        src, snp, dec = (os.path.join(d, x) for x in ("in", "in.snp", "in.dec"))
+        open(src, "wb").write(data)
+        subprocess.run([exe, "-c", "-i", src, snp], check=True, capture_output=True)
+        stream = open(snp, "rb").read()
+        assert stream == oracle.compress(data)
+        n, ent = snappy_amd.read_index(open(snp + ".idx", "rb").read())
+        assert n == len(data)
+        codec = snappy_amd.Codec(0)
+        try:
+            dn, offs = codec.index_tensor(torch.from_numpy(np.frombuffer(stream, dtype=np.uint8).copy()).cuda())
+        finally:
+            codec.close()
+        assert dn == len(data) and ent == [int(v) for v in offs.cpu().numpy()]
+        subprocess.run([exe, "-d", "-i", snp, dec], check=True, capture_output=True)
+        assert open(dec, "rb").read() == data
+        # a foreign index: refused, nothing decoded from it
+        other = oracle.compress(data[:-1])
+        open(snp, "wb").write(other)
+        r = subprocess.run([exe, "-d", "-i", snp, dec], capture_output=True)
+        assert r.returncode != 0
+
+
+def test_decompress_with_sidecar_index_xblock(codec, golden):
+    """A sidecar index with straddle entries (from the GPU index pass) drives
+    the host decoder of the cross-block vectors."""
+    import torch
+    for v in golden["xblock_vectors"][:6]:
+        stream = _xblock_stream(v)
+        n, offs = codec.index_tensor(torch.from_numpy(np.frombuffer(stream, dtype=np.uint8).copy()).cuda())
+        idx = _index_file(n, [int(x) for x in offs.cpu().numpy()])
+        out = snappy_amd.decompress_indexed(stream, idx)
+        assert sha(out) == v["out_sha256"], v["name"]

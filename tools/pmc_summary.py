@@ -1,43 +1,74 @@
 #!/usr/bin/env python3
 """Turn the rocprofv3 passes of tools/profile_round.sh into profiles/:
-  <round>_kernel_stats.csv  (copy of --kernel-trace --stats summary)
-  <round>_pmc.json          (HBM bytes per launch per kernel, corrected)
-  pmc_latest.json           (same, read by bench.py for roofline.traffic)
+  <round>_<W>_bench.json        the bench.py line
+  <round>_<W>_kernel_stats.csv  copy of the --kernel-trace --stats summary
+  <round>_<W>_pmc.json          per kernel and launch: HBM bytes (FETCH_SIZE,
+                                WRITE_SIZE, corrected) and the SQ counters
+  pmc_<W>.json                  same, read by bench.py for roofline.traffic
 Correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE/WRITE_SIZE are in
-KiB; on gfx950 FETCH_SIZE reports half the bytes of a coalesced streaming
-read, so it is doubled; WRITE_SIZE is taken as is."""
-import csv, json, os, shutil, sys
+KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced streaming
+read, so it is doubled; WRITE_SIZE is taken as is.  Other access widths are
+uncalibrated (the guide says so): the K1r/K2/K4 byte loads make `fetch_bytes`
+an estimate, exact only up to that factor.
+Usage: tools/pmc_summary.py [gpurun_out/prof] [round]"""
+import csv
+import json
+import os
+import shutil
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out")
-rnd = sys.argv[2] if len(sys.argv) > 2 else "r01"
-workload = sys.argv[3] if len(sys.argv) > 3 else "text32k"
+src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "prof")
+rnd = sys.argv[2] if len(sys.argv) > 2 else "r02"
 out = os.path.join(ROOT, "profiles")
 os.makedirs(out, exist_ok=True)
-shutil.copyfile(os.path.join(src, "prof_trace", "run_kernel_stats.csv"), os.path.join(out, f"{rnd}_kernel_stats.csv"))
 
 
-def per_kernel(path, counter):
+def per_kernel(path):
+    """{kernel: {counter: mean value per launch}}"""
     agg = {}
+    if not os.path.exists(path):
+        return {}
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter:
-            continue
         k = r["Kernel_Name"].split("(")[0].replace("snappy_amd::", "")
-        agg.setdefault(k, []).append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}
+        agg.setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in agg.items()}
 
 
-fetch = per_kernel(os.path.join(src, "prof_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
-write = per_kernel(os.path.join(src, "prof_write", "run_counter_collection.csv"), "WRITE_SIZE")
-res = {"workload": workload, "bytes_per_gpu": 1 << 30, "round": rnd,
-       "note": "per launch; FETCH_SIZE KiB x1024 x2 (gfx950 half-count correction), WRITE_SIZE KiB x1024",
-       "kernels": {}}
-for k in sorted(set(fetch) | set(write)):
-    if not k.startswith("k"):
+for w in sorted(os.listdir(src)):
+    d = os.path.join(src, w)
+    bench = os.path.join(d, "bench.json")
+    if not os.path.exists(bench):
         continue
-    f = fetch.get(k, 0.0) * 1024 * 2
-    w = write.get(k, 0.0) * 1024
-    res["kernels"][k] = {"fetch_bytes": round(f), "write_bytes": round(w), "hbm_bytes": round(f + w)}
-for name in (f"{rnd}_pmc.json", "pmc_latest.json"):
-    json.dump(res, open(os.path.join(out, name), "w"), indent=1)
-print(json.dumps(res, indent=1))
+    lines = [l for l in open(bench) if l.startswith("{")]
+    if not lines:
+        continue
+    line = json.loads(lines[-1])
+    shutil.copyfile(bench, os.path.join(out, f"{rnd}_{w}_bench.json"))
+    stats = os.path.join(d, "trace", "run_kernel_stats.csv")
+    if os.path.exists(stats):
+        shutil.copyfile(stats, os.path.join(out, f"{rnd}_{w}_kernel_stats.csv"))
+    fetch = per_kernel(os.path.join(d, "fetch", "run_counter_collection.csv"))
+    write = per_kernel(os.path.join(d, "write", "run_counter_collection.csv"))
+    sq = per_kernel(os.path.join(d, "sq", "run_counter_collection.csv"))
+    n = line["config"]["bytes_per_gpu"]
+    res = {"workload": w, "bytes_per_gpu": n, "round": rnd,
+           "note": "per launch; FETCH_SIZE KiB x1024 x2 (gfx950 half-count correction), WRITE_SIZE KiB x1024; "
+                   "SQ_* as rocprofv3 reports them (SQ_WAVE_CYCLES/SQ_BUSY_CYCLES in quad-cycles per the guide)",
+           "kernels": {}}
+    for k in sorted(set(fetch) | set(write) | set(sq)):
+        if not k.startswith("k"):
+            continue
+        f = fetch.get(k, {}).get("FETCH_SIZE", 0.0) * 1024 * 2
+        wr = write.get(k, {}).get("WRITE_SIZE", 0.0) * 1024
+        e = {"fetch_bytes": round(f), "write_bytes": round(wr), "hbm_bytes": round(f + wr)}
+        for c, v in sorted(sq.get(k, {}).items()):
+            e[c] = round(v)
+        if e.get("SQ_WAVES"):
+            for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"):
+                if c in e:
+                    e[c + "_per_wave"] = round(e[c] / e["SQ_WAVES"], 1)
+        res["kernels"][k] = e
+    for name in (f"{rnd}_{w}_pmc.json", f"pmc_{w}.json"):
+        json.dump(res, open(os.path.join(out, name), "w"), indent=1)
+    print(w, json.dumps(res["kernels"], indent=None)[:2000])

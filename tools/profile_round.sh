@@ -1,18 +1,39 @@
 #!/bin/bash
 # Round profiling recipe (run on the GPU box from the repo root):
-#   1. bench.py default line                    -> gpurun_out/bench.json
-#   2. rocprofv3 --kernel-trace --stats, same command  -> gpurun_out/prof_trace/
-#   3. rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE (separate passes, kernel trace only)
-# Each GPU step has its own time limit; steps are chained with &&.
+#   tools/profile_round.sh [workload ...]      (default: every bench workload)
+# For each workload W, under gpurun_out/prof/W/:
+#   bench.json    the bench.py line (CPU baselines on a bounded sample)
+#   trace/        rocprofv3 --kernel-trace --stats of the same command
+#   fetch/ write/ rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE (separate passes, kernel trace only)
+#   sq/           rocprofv3 --pmc of 8 SQ counters (instruction mix, wave cycles)
+# tools/pmc_summary.py then writes profiles/<round>_W_*.  Every GPU step has its
+# own time limit; steps are chained with && so the first failure ends the run.
 set -o pipefail
 cd "$(dirname "$0")/.."
-mkdir -p gpurun_out
 export TMPDIR=/tmp
+WLS=${*:-"text32k text64k random repeat decode10g"}
 STEPS=${STEPS:-5}
-timeout -k 10 400 python bench.py --steps $STEPS --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err &&
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o run --output-format csv -- \
-    python3 bench.py --steps $STEPS --warmup 2 --no-cpu-baseline --no-host-e2e > gpurun_out/prof_trace.log 2>&1 &&
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/prof_fetch -o run --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-e2e > gpurun_out/prof_fetch.log 2>&1 &&
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/prof_write -o run --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-e2e > gpurun_out/prof_write.log 2>&1
+SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"
+run() {  # workload
+    local w=$1 d=gpurun_out/prof/$1 q="--workload $1 --no-cpu-baseline --no-host-e2e"
+    mkdir -p $d &&
+    echo "[$(date +%T)] $w: bench" &&
+    timeout -k 10 400 python3 bench.py --workload $w --steps $STEPS --warmup 2 --cpu-sample-bytes 268435456 \
+        > $d/bench.json 2> $d/bench.err &&
+    echo "[$(date +%T)] $w: kernel trace" &&
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $d/trace -o run --output-format csv -- \
+        python3 bench.py $q --steps $STEPS --warmup 2 > $d/trace.log 2>&1 &&
+    echo "[$(date +%T)] $w: FETCH_SIZE" &&
+    timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $d/fetch -o run --output-format csv -- \
+        python3 bench.py $q --steps 2 --warmup 1 > $d/fetch.log 2>&1 &&
+    echo "[$(date +%T)] $w: WRITE_SIZE" &&
+    timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $d/write -o run --output-format csv -- \
+        python3 bench.py $q --steps 2 --warmup 1 > $d/write.log 2>&1 &&
+    echo "[$(date +%T)] $w: SQ counters" &&
+    timeout -k 10 400 rocprofv3 --pmc $SQ --kernel-trace -d $d/sq -o run --output-format csv -- \
+        python3 bench.py $q --steps 2 --warmup 1 > $d/sq.log 2>&1
+}
+for w in $WLS; do
+    run $w || exit 1
+done
+echo "[$(date +%T)] done"

@@ -269,6 +269,7 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
 #define SNAPPY_K1R_WINDOW 4  // W-probe rounds
 #endif
 
+
 #if defined(SNAPPY_K1R_LSTAMPS)
 #define MSTAMP(var)                                                                         \
     do {                                                                                    \
@@ -589,10 +590,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 // probe k = lane - lane0 for k <= kcap: step 1 before it ((skip + k - 1) >> 5 == 1),
                 // predecessors within DMAX; inside the window and before is_block_end (m_win);
                 // the probe at skip + k == 64 (only when 64 - skip < DMAX) needs L - p_k >= 17
-                uint64_t valid;
-                if (__builtin_expect(skip <= 64 - DMAX, 1)) {  // skip is known before lane0
-                    valid = (((1ull << DMAX) - 1) << lane0) & m_win;
-                } else {
+                // (one-sided branch: the common case costs a compare and a branch)
+                uint64_t valid = (((1ull << DMAX) - 1) << lane0) & m_win;
+                if (__builtin_expect(skip > 64 - DMAX, 0)) {
                     const uint32_t kcap = 64 - skip;
                     valid = ((2ull << kcap) - 1) << lane0;
                     if (lane0 + kcap < 64) valid &= ~((1ull << (lane0 + kcap)) & ~m_win17);
@@ -640,17 +640,20 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #ifdef SNAPPY_K1R_STATS
                     n_probe += f - lane0 + 1;
 #endif
+                    // every path defines the deferred token (dkn says whether it counts):
+                    // no loop-carried "keep" value, so no register copies at the latch
+                    len = __builtin_elementwise_min(len, L - pf);  // the compare never runs past the block
+                    dka = pf | (len << 16);
+                    dkb = pf - c;
                     if (__builtin_expect(len >= 4, 1)) {
-                        len = __builtin_elementwise_min(len, L - pf);  // the compare never runs past the block
 #ifdef SNAPPY_K1R_STATS
                         n_match++;
 #endif
-                        dka = pf | (len << 16);
-                        dkb = pf - c;
                         dkn = 1;
                         np = pf + len;
                         skip = 32;
                     } else {  // tag collision: a miss (append_literal :283-287 steps by skip >> 5)
+                        dkn = 0;
                         if (f == lane0) {  // its p - 1, then p again (the later write wins)
                             TBL_WRITE3(lane - (lane0 - 1) <= 1 ? adr : kDummy, word);
                             LDS_ORDER();
@@ -660,6 +663,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     }
                 } else {
                     LSTAMP(s3);
+                    dka = dkb = dkn = 0;
                     const uint32_t nk = (uint32_t)__builtin_popcountll(valid);  // lanes lane0 .. lane0 + nk - 1
                     // update_hash_table :303-307: p_k - 1 and p_k of every miss, lane order
                     TBL_WRITE3(lane - (lane0 - 1) <= nk ? adr : kDummy, word);

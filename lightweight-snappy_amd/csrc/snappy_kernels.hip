@@ -386,15 +386,52 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         else g3[i - 96] = w;
     }
 
-    // BIG: segments [seg_hi - 128, seg_hi) are resident in the ring registers
+    // BIG: segments [seg_hi - 128, seg_hi) are resident in the ring registers;
+    // segment seg_hi is prefetched into LDS by an LDS-DMA load (global_load_lds)
+    // as soon as the ring moves, so the next advance finds it there instead of
+    // waiting on a global load
     uint32_t seg_hi = kRegs;
-    // make segments < need resident (a long jump reloads at most the last 128)
-    auto ring_to = [&](uint32_t need) {
+    __shared__ uint32_t ring_stage[64];
+    uint32_t staged = 0;  // BIG: 1 + the segment in ring_stage, 0 = none
+    auto stage = [&](uint32_t sg) {
+        if constexpr (BIG) {
+            staged = 0;
+            if (aligned && 256 * (sg + 1) <= L) {
+                // scalar base + lane offset (the builtin would keep a 64-bit per-lane
+                // address live and spill); the compiler does not track this load:
+                // ring_to waits vmcnt(0) before the LDS read
+                const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)ring_stage;
+                // (lane offset computed inside: hoisted, it would hold a VGPR for the whole kernel)
+                uint32_t m0_save, voff;  // m0 is reserved to the compiler (writelane lane selects): restore it
+                asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\tv_lshlrev_b32 %1, 2, %3\n\t"
+                             "global_load_lds_dword %1, %4\n\ts_mov_b32 m0, %0"
+                             : "=&s"(m0_save), "=&v"(voff)
+                             : "s"(lds), "v"(lane), "s"(src + 256 * sg)
+                             : "memory");
+                staged = sg + 1;
+            }
+        }
+    };
+    stage(seg_hi);
+    // make segments < need resident (a long jump reloads at most the last 128).
+    // PF (the window refresh, which moves the ring one segment at a time): take
+    // the staged segment and stage the next; match extension loads directly.
+    auto ring_to = [&](uint32_t need, auto pf) {
         if constexpr (BIG) {
             if (__builtin_expect(need <= seg_hi, 1)) return;
-            for (uint32_t sg = need - seg_hi > kRegs ? need - kRegs : seg_hi; sg < need; sg++)
-                REG_SET_V(sg & (kRegs - 1), load_word(sg));
+            uint32_t sg = need - seg_hi > kRegs ? need - kRegs : seg_hi;
+            if (decltype(pf)::value && staged == sg + 1) {  // the DMA was issued an advance ago
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)ring_stage;
+                uint32_t w;
+                asm volatile("v_lshl_add_u32 %0, %1, 2, %2\n\tds_read_b32 %0, %0\n\ts_waitcnt lgkmcnt(0)"
+                             : "=&v"(w) : "v"(lane), "s"(lds) : "memory");
+                REG_SET_V(sg & (kRegs - 1), __builtin_bswap32(w));
+                sg++;
+            }
+            for (; sg < need; sg++) REG_SET_V(sg & (kRegs - 1), load_word(sg));
             seg_hi = need;
+            if (decltype(pf)::value) stage(seg_hi);  // REG_SET_V consumed the LDS read: the DMA may overwrite it
         }
     };
     // lane i <- big-endian dword dd + i: from the registers, or (BIG, a segment
@@ -459,7 +496,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #define WINDOW_AT(qq)                                                                              \
     do {                                                                                           \
         q0 = (qq);                                                                                 \
-        ring_to((q0 >> 8) + 2); /* BIG: the window's segments and the next */                      \
+        ring_to((q0 >> 8) + 2, std::true_type{}); /* BIG: the window's segments and the next */    \
         d0 = q0 >> 2;                                                                              \
         dr = d0 & 63;                                                                              \
         {                                                                                          \
@@ -500,7 +537,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             for (;;) {
                 if (pf + len >= L) break;
                 const uint32_t qa = pf + len, qb = cand + len;
-                ring_to((qa >> 8) + 2);
+                ring_to((qa >> 8) + 2, std::false_type{});
                 const uint32_t a0 = DW_LANES(qa >> 2), b0 = CAND_LANES(qb >> 2);
                 const uint32_t va = funnel_bytes(a0, wave_shl1(a0), perm_sel(qa & 3));
                 const uint32_t vb = funnel_bytes(b0, wave_shl1(b0), perm_sel(qb & 3));

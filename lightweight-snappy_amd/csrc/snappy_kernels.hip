@@ -1478,7 +1478,7 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
 
 #ifdef SNAPPY_K4_STATS
     const uint64_t t_loop = clock64();
-    uint32_t n_el = 0, n_batch = 0, n_pass = 0, n_sub = 0;
+    uint32_t n_el = 0, n_batch = 0, n_pass = 0, n_sub = 0, n_far = 0;
     uint64_t sg0 = 0, sg1 = 0, sg2 = 0, ta, tb, tc, td;
 #endif
     // [cur | nxt] byte-window gathers (q per lane, < 512)
@@ -1731,6 +1731,7 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                     pend = pend && !rdy;
 #ifdef SNAPPY_K4_STATS
                     n_sub++;
+                    n_far += __ballot(rdy && !lit && src < (SrcT)lo) != 0;
 #endif
                     if (!__ballot(pend)) break;
                 }
@@ -1767,7 +1768,7 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     if (lane == 0 && u < 32768) {
         uint64_t *g = g_k4_stats + 8 * u;
         g[0] = clock64() - t_loop;
-        g[1] = n_el;
+        g[1] = n_el | ((uint64_t)n_far << 32);
         g[2] = n_batch;
         g[3] = n_pass;
         g[4] = n_sub;

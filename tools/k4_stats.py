@@ -18,9 +18,13 @@ buf = np.zeros(units * 8, dtype=np.uint64)
 lib = snappy_amd.lib()
 lib.snappy_amd_debug_k4_stats.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 assert lib.snappy_amd_debug_k4_stats(buf.ctypes.data_as(ctypes.c_void_p), units * 8) == 0
-st = buf.reshape(units, 8).astype(np.float64)
+st = buf.reshape(units, 8)
+far = (st[:, 1] >> 32).astype(np.float64)
+st = st.astype(np.float64)
+st[:, 1] = (buf.reshape(units, 8)[:, 1] & 0xFFFFFFFF).astype(np.float64)
 m = st.mean(axis=0)
-print(f"{kind} units {units}: elements/unit {m[1]:.0f} batches {m[2]:.0f} passes {m[3]:.0f} subpasses {m[4]:.0f}")
+print(f"{kind} units {units}: elements/unit {m[1]:.0f} batches {m[2]:.0f} passes {m[3]:.0f} subpasses {m[4]:.0f}"
+      f" sub-passes reading HBM (copies beyond the ring) {far.mean():.0f}")
 print(f"cycles/unit {m[0]:.0f}  cycles/element {m[0]/m[1]:.1f}  cycles/batch {m[0]/m[2]:.0f}")
 for i, nm in ((5, "window+candidate parse"), (6, "doubling+gather+scans+validate"), (7, "execute (passes)")):
     print(f"  {nm:32s} {m[i]/m[2]:7.0f} cycles/batch  {100*m[i]/m[0]:5.1f}%")

@@ -1708,6 +1708,12 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 const uint32_t o = P + lane;
                 const bool lit = (f_op >> 31) != 0;
                 uint32_t d = o - (f_op & 0x7FFFFFFFu);
+                // a far source (below lo: only in HBM) never overlaps its copy (off >
+                // ring - 64 > len): its load is issued before the window gather
+                const SrcT src0 = (SrcT)(f_op & 0x7FFFFFFFu) - (SrcT)f_in + (SrcT)d;
+                bool farl = !lit && o < op_end && src0 < (SrcT)lo;
+                uint8_t fv = 0;
+                if (farl) fv = dst[src0];
                 // literal byte from the window (computed by every lane: bpermute needs them all)
                 const uint32_t q = (f_in + d) & 511;
                 const uint32_t lw = WIN_DW(q >> 2);
@@ -1719,19 +1725,37 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 }
                 const SrcT src = (SrcT)(f_op & 0x7FFFFFFFu) - (SrcT)f_in + (SrcT)d;
                 bool pend = o < op_end;
+                if constexpr (BACK) {
+                    // an overlapping copy near the unit start may repeat bytes of an earlier unit
+                    if (!lit && pend && !farl && src < (SrcT)lo) {
+                        fv = dst[src];
+                        farl = true;
+                    }
+                }
+                // the common pass: no byte depends on another byte of the same pass
+                if (!__ballot(pend && !lit && src >= (SrcT)P)) {
+                    if (pend) ob[o & M] = lit ? lb : (farl ? fv : ob[(uint32_t)src & M]);
+#ifdef SNAPPY_K4_STATS
+                    n_sub++;
+                    n_pass++;
+                    n_far += __ballot(farl) != 0;
+#endif
+                    continue;
+                }
+                // else sub-passes: a byte is written once its source byte has been
                 uint64_t written = 0;
                 for (;;) {
                     const bool rdy = pend && (lit || src < (SrcT)P || ((written >> ((uint32_t)(src - (SrcT)P) & 63)) & 1));
                     if (rdy) {
                         uint8_t v = lb;
-                        if (!lit) v = src >= (SrcT)lo ? ob[(uint32_t)src & M] : dst[src];
+                        if (!lit) v = farl ? fv : ob[(uint32_t)src & M];
                         ob[o & M] = v;
                     }
                     written |= __ballot(rdy);
                     pend = pend && !rdy;
 #ifdef SNAPPY_K4_STATS
                     n_sub++;
-                    n_far += __ballot(rdy && !lit && src < (SrcT)lo) != 0;
+                    n_far += __ballot(rdy && farl) != 0;
 #endif
                     if (!__ballot(pend)) break;
                 }

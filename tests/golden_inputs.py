@@ -158,6 +158,10 @@ def decoder_vector_ops() -> dict:
         "straddle_copy": [["lit", B - 10, 21], ["copy", 40, 1000, 2], ["lit", 50, 22]],
         "straddle_copy_overlap": [["lit", B - 3, 23], ["copy", 64, 3, 2], ["copy", 11, 2, 1]],
         "straddle_copy4": [["lit", B - 1, 24], ["copy", 2, 1, 4], ["lit", 9, 25]],
+        # overlapping copies (offset < length) just after the boundary: the
+        # repeated bytes lie in the earlier block
+        "xblock_copy_overlap": [["lit", B + 2, 29], ["copy", 60, 5, 2], ["copy", 9, 7, 1], ["lit", 3, 30]],
+        "xblock_copy1_overlap": [["lit", B, 31], ["copy", 11, 4, 1], ["copy", 64, 1, 2]],
         # a literal covering a whole block (block 1 starts and ends inside it)
         "literal_spans_3_blocks": [["lit", 1000, 26], ["lit", 131000, 27, 3], ["copy", 64, 131072, 4]],
         # every block copies from the previous one: a pass-2 dependency chain

@@ -10,6 +10,4 @@ mkdir -p /tmp/isa
 /opt/rocm/lib/llvm/bin/clang-offload-bundler --unbundle --type=o --input=/tmp/isa/k.bundle \
     --targets=hipv4-amdgcn-amd-amdhsa--gfx950 --output=/tmp/isa/k.co
 /opt/rocm/lib/llvm/bin/llvm-objdump -d /tmp/isa/k.co > /tmp/isa/k.s
-/opt/rocm/lib/llvm/bin/llvm-readobj --notes /tmp/isa/k.co |
-    grep -E "^ +\.(name|vgpr_count|sgpr_count|agpr_count|group_segment_fixed_size|vgpr_spill_count|sgpr_spill_count):" |
-    awk '{printf "%s%s", $0, (++i % 7 ? "" : "\n")}' | sed 's/  */ /g'
+/opt/rocm/lib/llvm/bin/llvm-readobj --notes /tmp/isa/k.co | python3 tools/kres.py

@@ -872,18 +872,6 @@ __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v, uint32_t *total
     return x - v;
 }
 
-// wave-wide OR, uniform result
-__device__ __forceinline__ uint32_t wave_or(uint32_t x)
-{
-    x |= dpp0<0x111, 0xF>(x);
-    x |= dpp0<0x112, 0xF>(x);
-    x |= dpp0<0x114, 0xF>(x);
-    x |= dpp0<0x118, 0xF>(x);
-    x |= dpp0<0x142, 0xA>(x);
-    x |= dpp0<0x143, 0xC>(x);
-    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-}
-
 template <typename P>
 __device__ __forceinline__ void put_copy(P *o, uint32_t len, uint32_t off)
 {
@@ -1509,10 +1497,9 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
         const uint32_t kq = ((o & 3) + lane) >> 2;
         const uint32_t dA = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(kq << 2), (int)w64);
         const uint32_t dB = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((kq + 1) << 2), (int)w64);
-        const uint32_t dC = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((kq + 2) << 2), (int)w64);
         const uint32_t sh = 8 * (q & 3);
         const uint32_t x0 = sh ? (dA >> sh) | (dB << (32 - sh)) : dA;  // tag, t1, t2, t3
-        const uint32_t x1 = sh ? (dB >> sh) | (dC << (32 - sh)) : dB;  // t4..t7
+        const uint32_t x1 = dB >> sh;  // t4 in bits 0..7 (the only byte used: b4 below)
         const uint32_t tag = x0 & 0xFF;
         uint32_t size, olen, info;  // info: copy offset, or literal header length
         const uint32_t t = tag & 3;
@@ -1674,35 +1661,22 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             const bool ex = lane < nexec;
             const uint32_t kop = e_op | (e_t == 0 ? 0x80000000u : 0u);
             const uint32_t kinfo = e_t == 0 ? e_lsrc : e_info;
-#ifdef SNAPPY_K4_BITMAP
-            const uint32_t mlo = lane >= 31 ? 0xFFFFFFFFu : (2u << lane) - 1;
-            const uint32_t mhi = lane < 32 ? 0u : (lane == 63 ? 0xFFFFFFFFu : (2u << (lane - 32)) - 1);
-#endif
             for (uint32_t P = op; P < op_end; P += 64) {
                 const uint32_t j = e_op - P;
                 const bool inw = ex && j < 64;
                 const uint32_t cb = (uint32_t)__builtin_popcountll(__ballot(ex && e_op < P));
-#ifdef SNAPPY_K4_BITMAP
-                const uint32_t slo = wave_or(inw && j < 32 ? 1u << (j & 31) : 0u);
-                const uint32_t shi = wave_or(inw && j >= 32 ? 1u << (j & 31) : 0u);
-                const uint32_t id = cb + __builtin_popcount(slo & mlo) + __builtin_popcount(shi & mhi) - 1;
-#else
-                // scatter (element index + 1) onto the byte lane where it starts:
-                // ds_permute delivers 0 to untargeted lanes and the highest sender
-                // wins a collision, so the element lanes are first reversed around
-                // cb (the pass's elements land on the highest lanes; every other
-                // lane sends 0); an inclusive max-scan then gives each byte's element
-                const uint32_t pk = (j & 63) | (inw ? (lane + 1) << 8 : 0u);
+                // the pass's element starts as a lane mask: the element lanes are
+                // reversed around cb so that the pass's elements are the highest
+                // lanes (every other lane sends 0, and ds_permute keeps the highest
+                // sender of a collision and gives 0 to lanes nobody targets), then
+                // each element sends 1 to the byte lane where it starts; a byte's
+                // element = the elements before the pass + the starts at or below it
+                const uint32_t pk = (j & 63) | (inw ? 0x100u : 0u);
                 const uint32_t rv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((cb + 63 - lane) & 63) << 2), (int)pk);
-                uint32_t mk = (uint32_t)__builtin_amdgcn_ds_permute((int)((rv & 63) << 2), (int)(rv >> 8));
-                mk = __builtin_elementwise_max(mk, dpp0<0x111, 0xF>(mk));
-                mk = __builtin_elementwise_max(mk, dpp0<0x112, 0xF>(mk));
-                mk = __builtin_elementwise_max(mk, dpp0<0x114, 0xF>(mk));
-                mk = __builtin_elementwise_max(mk, dpp0<0x118, 0xF>(mk));
-                mk = __builtin_elementwise_max(mk, dpp0<0x142, 0xA>(mk));
-                mk = __builtin_elementwise_max(mk, dpp0<0x143, 0xC>(mk));
-                const uint32_t id = (mk > cb ? mk : cb) - 1;
-#endif
+                const uint32_t fl = (uint32_t)__builtin_amdgcn_ds_permute((int)((rv & 63) << 2), (int)(rv >> 8));
+                const uint64_t sm = __ballot(fl != 0);
+                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+                const uint32_t id = cb + below + (fl != 0 ? 1u : 0u) - 1;
                 const uint32_t f_op = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((id & 63) << 2), (int)kop);
                 const uint32_t f_in = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((id & 63) << 2), (int)kinfo);
                 const uint32_t o = P + lane;

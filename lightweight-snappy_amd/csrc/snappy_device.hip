@@ -277,16 +277,16 @@ static int decompress_launch(snappy_amd_ctx *c, const void *d_comp, const uint64
     if (allow_back) HIP_OK(hipMemsetAsync(c->status + units, 0, 2 * sizeof(int32_t), c->stream));
     const uint32_t ring = k4_ring_bytes(unit);
     const uint32_t hm = hdr_mode_of(layout, flags);
-    // dynamic LDS: the ring + 16 bytes of per-unit scalars
+    // dynamic LDS: the ring + per-unit scalars + the compressed-input window
     // the kernel reads aligned dwords: pass the stream as an aligned base + bias
     const uint32_t bias = (uint32_t)(reinterpret_cast<uintptr_t>(d_comp) & 3);
     const uint8_t *comp = static_cast<const uint8_t *>(d_comp) - bias;
-    hipLaunchKernelGGL(k4_decompress_units, dim3((uint32_t)units), dim3(64), ring + 16, c->stream, comp, d_offsets,
+    hipLaunchKernelGGL(k4_decompress_units, dim3((uint32_t)units), dim3(64), ring + SNAPPY_K4_LDS_EXTRA, c->stream, comp, d_offsets,
                        (uint64_t)n, unit, hm, header_value, ring, allow_back, bias, static_cast<uint8_t *>(d_out),
                        c->status);
     HIP_OK(hipGetLastError());
     if (allow_back) {
-        hipLaunchKernelGGL(k4_decompress_back, dim3((uint32_t)units), dim3(64), ring + 16, c->stream, comp,
+        hipLaunchKernelGGL(k4_decompress_back, dim3((uint32_t)units), dim3(64), ring + SNAPPY_K4_LDS_EXTRA, c->stream, comp,
                            d_offsets, (uint64_t)n, unit, hm, header_value, ring, bias, static_cast<uint8_t *>(d_out),
                            c->status);
         HIP_OK(hipGetLastError());

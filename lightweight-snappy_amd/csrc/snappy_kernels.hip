@@ -1215,8 +1215,9 @@ __global__ __launch_bounds__(1024) void k3_scan(const uint32_t *__restrict__ siz
 
 // ---------------------------------------------------------------------------
 // K4: one wave per unit.  The compressed unit streams through a 512-byte
-// register window (cur = bytes [B, B+256), nxt = [B+256, B+512), one dword
-// per lane, nxt prefetched a window ahead).  Each batch parses the elements
+// window in LDS (three 256-byte slots used round robin, the next segment
+// prefetched into a register a slide ahead), so a lane reads its candidate
+// element's bytes, or a literal byte, with one LDS read.  Each batch parses the elements
 // starting in the next 64 window bytes lane-parallel (tag dispatch of
 // src/snappy_decompression.c:290-333, element chain by pointer doubling),
 // then executes them in 64-byte output passes into an LDS ring that is
@@ -1391,13 +1392,34 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
         tail_lds[1] = want - skip1;
     }
 
-    // register window over the compressed unit (absolute 4-aligned base B)
+    // LDS window over the compressed unit: 3 slots of 256 bytes (after the ring
+    // and the tail scalars) + a 16-byte mirror of slot 0's head, so an 8-byte
+    // read crossing from slot 2 into slot 0 stays contiguous.  The window is the
+    // 512 bytes from the absolute 4-aligned base B: its first 256 in slot ws, the
+    // next in slot (ws + 1) % 3; the segment after that is prefetched into `pre`
+    // (a register) and written to the free slot when the window slides.
+    auto *const wb = (__attribute__((address_space(3))) uint8_t *)(lds + ring / 4 + 4);
+    auto *const w32 = reinterpret_cast<__attribute__((address_space(3))) uint32_t *>(wb);
     uint64_t B = c0 & ~3ull;
-    uint32_t cur = load_dw_guarded(comp, B + 4 * lane, c0 + clen);
-    uint32_t nxt = load_dw_guarded(comp, B + 256 + 4 * lane, c0 + clen);
     c1 = c0 + clen;
-    // dword k (0..127) of [cur | nxt], k uniform
-#define WDW(k) ((uint32_t)((k) < 64 ? __builtin_amdgcn_readlane(cur, (k)) : __builtin_amdgcn_readlane(nxt, (k) - 64)))
+    uint32_t ws = 0;
+    // window byte x (< 512 + 8) -> LDS byte address in wb
+#define WADR(x) ({ const uint32_t _a = 256 * ws + (x); _a >= 768 ? _a - 768 : _a; })
+    auto put_seg = [&](uint32_t slot, uint32_t v) {
+        w32[64 * slot + lane] = v;
+        if (slot == 0 && lane < 4) w32[192 + lane] = v;  // the mirror
+    };
+    uint32_t pre;
+    {
+        const uint32_t w0 = load_dw_guarded(comp, B + 4 * lane, c1);
+        const uint32_t w1 = load_dw_guarded(comp, B + 256 + 4 * lane, c1);
+        pre = load_dw_guarded(comp, B + 512 + 4 * lane, c1);
+        put_seg(0, w0);
+        put_seg(1, w1);
+        __builtin_amdgcn_wave_barrier();
+    }
+    // dword k (0..127) of the window at its start (ws = 0), k uniform
+#define WDW(k) rfl(w32[k])
 
     uint32_t ip = 0, op = 0;  // ip relative to c0
     // varint preamble: every STREAMS unit, and block 0 of a SINGLE stream
@@ -1469,35 +1491,32 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     uint32_t n_el = 0, n_batch = 0, n_pass = 0, n_sub = 0, n_far = 0;
     uint64_t sg0 = 0, sg1 = 0, sg2 = 0, ta, tb, tc, td;
 #endif
-    // [cur | nxt] byte-window gathers (q per lane, < 512)
-#define WIN_DW(qd) ({ const uint32_t _qd = (qd);                                                     \
-        const uint32_t _a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_qd & 63) << 2), (int)cur);   \
-        const uint32_t _b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_qd & 63) << 2), (int)nxt);   \
-        _qd < 64 ? _a : _b; })
     while (st == SNAPPY_ST_OK && op < want) {
         if (ip >= clen) { st = SNAPPY_ST_TRUNCATED; break; }
         K4STAMP(ta);
         uint32_t o = (uint32_t)(c0 + ip - B);
         if (o >= 256) {
-            if (o < 512) {  // slide the window by 256 bytes, prefetch the next one
+            if (o < 512) {  // slide by 256 bytes: the prefetched segment fills the free slot
                 B += 256;
-                cur = nxt;
                 o -= 256;
+                ws = ws == 2 ? 0 : ws + 1;
+                put_seg(ws == 2 ? 0 : ws + 1, pre);
             } else {  // jumped past the window (long literal): restart it here
                 B = (c0 + ip) & ~3ull;
-                cur = load_dw_guarded(comp, B + 4 * lane, c1);
                 o = (uint32_t)(c0 + ip - B);
+                ws = 0;
+                put_seg(0, load_dw_guarded(comp, B + 4 * lane, c1));
+                put_seg(1, load_dw_guarded(comp, B + 256 + 4 * lane, c1));
             }
-            nxt = load_dw_guarded(comp, B + 256 + 4 * lane, c1);
+            __builtin_amdgcn_wave_barrier();
+            pre = load_dw_guarded(comp, B + 512 + 4 * lane, c1);
         }
         // ---- lane-parallel candidate parse: an element starting at o + lane
         const uint32_t q = o + lane;  // < 320
-        // the 64 dwords from o / 4 once, then each lane's three
-        const uint32_t w64 = WIN_DW((o >> 2) + lane);
-        const uint32_t kq = ((o & 3) + lane) >> 2;
-        const uint32_t dA = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(kq << 2), (int)w64);
-        const uint32_t dB = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((kq + 1) << 2), (int)w64);
-        const uint32_t sh = 8 * (q & 3);
+        const uint32_t qa = WADR(q);
+        // two aligned dwords (one ds_read2_b32; unaligned LDS reads measured slower)
+        const uint32_t dA = w32[qa >> 2], dB = w32[(qa >> 2) + 1];
+        const uint32_t sh = 8 * (qa & 3);
         const uint32_t x0 = sh ? (dA >> sh) | (dB << (32 - sh)) : dA;  // tag, t1, t2, t3
         const uint32_t x1 = dB >> sh;  // t4 in bits 0..7 (the only byte used: b4 below)
         const uint32_t tag = x0 & 0xFF;
@@ -1688,10 +1707,8 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 bool farl = !lit && o < op_end && src0 < (SrcT)lo;
                 uint8_t fv = 0;
                 if (farl) fv = dst[src0];
-                // literal byte from the window (computed by every lane: bpermute needs them all)
-                const uint32_t q = (f_in + d) & 511;
-                const uint32_t lw = WIN_DW(q >> 2);
-                const uint8_t lb = (uint8_t)(lw >> (8 * (q & 3)));
+                // literal byte from the window (read by every lane: garbage for copies)
+                const uint8_t lb = wb[WADR((f_in + d) & 511)];
                 if (!lit && d >= f_in && f_in) {  // overlapping copy (off < len <= 64)
                     const float r = __builtin_amdgcn_rcpf((float)f_in);
                     const uint32_t qd = (uint32_t)((float)d * r + 0.0001f);
@@ -1760,7 +1777,7 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             st = SNAPPY_ST_TRUNCATED;  // no progress possible
         }
     }
-#undef WIN_DW
+#undef WADR
 #undef WDW
 #ifdef SNAPPY_K4_STATS
     if (lane == 0 && u < 32768) {

@@ -459,7 +459,11 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     for (uint32_t i = lane; i < kTable; i += 64) TBL_WRITE(i, init);
     __syncthreads();
 
-    uint2 *tok = tokens + (uint64_t)u * tok_cap;
+    // tokens, structure of arrays (6 bytes each): position | length << 16 as
+    // u32, the copy offset (< 65,536) as u16 after all units' u32 words
+    uint32_t *tok = reinterpret_cast<uint32_t *>(tokens) + (uint64_t)u * tok_cap;
+    uint16_t *tok_off = reinterpret_cast<uint16_t *>(reinterpret_cast<uint32_t *>(tokens) +
+                                                     (uint64_t)gridDim.x * tok_cap) + (uint64_t)u * tok_cap;
     uint32_t tka = 0, tkb = 0;  // pending tokens: lane t < pend holds token nt + t
     uint32_t nt = 0, pend = 0;
     // encoded size so far (header, literals, copies: src/snappy_compression.c:95-165)
@@ -470,7 +474,10 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     uint32_t *const segu = seg_off + (uint64_t)u * segs;
     auto flush_tokens = [&]() {
         const bool has = lane < pend;
-        if (has) tok[nt + lane] = make_uint2(tka, tkb);
+        if (has) {
+            tok[nt + lane] = tka;
+            tok_off[nt + lane] = (uint16_t)tkb;
+        }
         const uint32_t pos = tka & 0xFFFF, len = tka >> 16, end = pos + len;
         // lane l <- end of lane l - 1; lane 0 keeps cend (no bound_ctrl: the old value stays)
         const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp((int)cend, (int)end, 0x138, 0xF, 0xF, false);
@@ -1078,7 +1085,9 @@ __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(cons
     const uint32_t L = (uint32_t)((n - base) < unit ? (n - base) : unit);
     const uint8_t *src = in + base;
     uint8_t *dst = out + offsets[u];
-    const uint2 *tok = tokens + (uint64_t)u * tok_cap;
+    const uint32_t *tok = reinterpret_cast<const uint32_t *>(tokens) + (uint64_t)u * tok_cap;
+    const uint16_t *tok_off = reinterpret_cast<const uint16_t *>(reinterpret_cast<const uint32_t *>(tokens) +
+                                                                 (uint64_t)gridDim.x * tok_cap) + (uint64_t)u * tok_cap;
     if (blockIdx.y == 0) {
         if (hdr_mode == SNAPPY_HDR_EVERY_UNIT) varint_put(L, dst, lane);
         else if (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0) varint_put(header_value, dst, lane);
@@ -1089,8 +1098,8 @@ __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(cons
     // end of the previous segment's last token = start of this segment's first literal
     uint32_t carry = 0;
     if (c) {
-        const uint2 k = tok[c - 1];
-        carry = (k.x & 0xFFFF) + (k.x >> 16);
+        const uint32_t k = tok[c - 1];
+        carry = (k & 0xFFFF) + (k >> 16);
     }
 
     uint32_t pos[kK2Per], len[kK2Per], off[kK2Per], pe[kK2Per], litn[kK2Per], hl[kK2Per], sz[kK2Per];
@@ -1101,10 +1110,10 @@ __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(cons
         pos[i] = L; len[i] = 0; off[i] = 0;  // pseudo-token: tail literal
         live[i] = t <= nt;
         if (t < nt) {
-            const uint2 k = tok[t];
-            pos[i] = k.x & 0xFFFF;
-            len[i] = k.x >> 16;
-            off[i] = k.y;
+            const uint32_t k = tok[t];
+            pos[i] = k & 0xFFFF;
+            len[i] = k >> 16;
+            off[i] = tok_off[t];
             if (len[i] == 0) len[i] = 65536;  // unreachable for units <= 32 KiB
         }
     }

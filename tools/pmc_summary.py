@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Turn the rocprofv3 passes of tools/profile_round.sh into profiles/:
-  <round>_<W>_bench.json        the bench.py line
+  <round>_<W>_bench.json        the bench.py line (roofline.traffic from this round's passes)
   <round>_<W>_kernel_stats.csv  copy of the --kernel-trace --stats summary
   <round>_<W>_pmc.json          per kernel and launch: HBM bytes (FETCH_SIZE,
                                 WRITE_SIZE, corrected) and the SQ counters
@@ -71,4 +71,12 @@ for w in sorted(os.listdir(src)):
         res["kernels"][k] = e
     for name in (f"{rnd}_{w}_pmc.json", f"pmc_{w}.json"):
         json.dump(res, open(os.path.join(out, name), "w"), indent=1)
+    # the bench line ran before these passes (it read the previous pmc_<W>.json):
+    # give its roofline the traffic measured now on the same code and workload
+    k = line.get("roofline", {}).get("kernel")
+    if k in res["kernels"]:
+        line["roofline"]["traffic"] = res["kernels"][k]["hbm_bytes"]
+        line["roofline"]["traffic_source"] = f"profiles/{rnd}_{w}_pmc.json"
+        with open(os.path.join(out, f"{rnd}_{w}_bench.json"), "w") as f:
+            f.write(json.dumps(line) + "\n")
     print(w, json.dumps(res["kernels"], indent=None)[:2000])

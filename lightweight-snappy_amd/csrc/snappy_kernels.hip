@@ -20,6 +20,16 @@
 
 #include "snappy_kernels.h"
 
+// The Makefile builds this file twice: SNAPPY_TU=1 emits the compress kernels
+// (K1r, K2, K3), SNAPPY_TU=2 the decode kernels (K4, K5), so each object is
+// compiled with the instruction scheduler measured fastest for its kernels.
+// SNAPPY_TU unset (tools/isa.sh, variant builds) emits all of them.
+#ifndef SNAPPY_TU
+#define SNAPPY_TU 0
+#endif
+#define SNAPPY_TU_COMPRESS (SNAPPY_TU != 2)
+#define SNAPPY_TU_DECODE (SNAPPY_TU != 1)
+
 namespace snappy_amd {
 
 // v_writelane_b32 (no clang builtin in this toolchain): the LLVM intrinsic by name
@@ -837,6 +847,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #endif
 }
 
+#if SNAPPY_TU_COMPRESS
 __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
                                                           uint32_t hdr_mode, uint64_t header_value,
                                                           uint2 *__restrict__ tokens, uint32_t tok_cap,
@@ -846,9 +857,11 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units(const uint8_t *__restri
 {
     k1r_body<false>(in, n, unit, hdr_mode, header_value, tokens, tok_cap, ntok_out, sizes, seg_off, segs);
 }
+#endif
 
 // 65,536-byte blocks (the reference's MAX_BLOCK_SIZE): a 32 KiB register
 // ring over the block, three waves per SIMD
+#if SNAPPY_TU_COMPRESS
 __global__ __launch_bounds__(64, 3) void k1r_match_units64(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
                                                             uint32_t hdr_mode, uint64_t header_value,
                                                             uint2 *__restrict__ tokens, uint32_t tok_cap,
@@ -858,6 +871,7 @@ __global__ __launch_bounds__(64, 3) void k1r_match_units64(const uint8_t *__rest
 {
     k1r_body<true>(in, n, unit, hdr_mode, header_value, tokens, tok_cap, ntok_out, sizes, seg_off, segs);
 }
+#endif
 
 // ---------------------------------------------------------------------------
 // K2: token list -> Snappy bytes at the unit's final offset (after K3's scan),
@@ -1069,6 +1083,7 @@ __device__ __forceinline__ void k2_long_literals(uint8_t *w, const uint8_t *__re
 #ifndef SNAPPY_K2_WAVES_PER_EU
 #define SNAPPY_K2_WAVES_PER_EU 1
 #endif
+#if SNAPPY_TU_COMPRESS
 __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
                                                     uint32_t hdr_mode, uint64_t header_value,
                                                     const uint2 *__restrict__ tokens, uint32_t tok_cap,
@@ -1164,6 +1179,7 @@ __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(cons
     __builtin_amdgcn_wave_barrier();  // the stage is reused by the next segment
     }
 }
+#endif
 
 // ---------------------------------------------------------------------------
 // K3a: exclusive scan of unit sizes -> offsets[0..count], total.
@@ -1173,8 +1189,9 @@ __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(cons
 // scans combine threads within a wave and the 16 wave totals.  A unit is at
 // most ~67.6 KB, so a tile's relative prefix fits 32 bits; the carry is 64-bit.
 constexpr uint32_t kScanPer = 8;
-constexpr uint32_t kScanTile = 1024 * kScanPer;
+[[maybe_unused]] constexpr uint32_t kScanTile = 1024 * kScanPer;
 
+#if SNAPPY_TU_COMPRESS
 __global__ __launch_bounds__(1024) void k3_scan(const uint32_t *__restrict__ sizes, uint64_t count,
                                                 uint64_t *__restrict__ offsets, uint64_t *__restrict__ total)
 {
@@ -1221,6 +1238,7 @@ __global__ __launch_bounds__(1024) void k3_scan(const uint32_t *__restrict__ siz
         *total = carry;
     }
 }
+#endif
 
 // ---------------------------------------------------------------------------
 // K4: one wave per unit.  The compressed unit streams through a 512-byte
@@ -1347,7 +1365,9 @@ __device__ __noinline__ int32_t k4_wait(const int32_t *status, uint64_t g_lo, ui
 }
 
 #ifdef SNAPPY_K4_STATS
+#if SNAPPY_TU_DECODE
 __device__ uint64_t g_k4_stats[32768 * 8];
+#endif
 #define K4STAMP(var)                                                                        \
     do {                                                                                    \
         __builtin_amdgcn_sched_barrier(0);                                                  \
@@ -1813,6 +1833,7 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     }
 }
 
+#if SNAPPY_TU_DECODE
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_decompress_units(
     const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets, uint64_t n, uint32_t unit,
     uint32_t hdr_mode, uint64_t header_value, uint32_t ring, uint32_t allow_back, uint32_t bias, uint8_t *__restrict__ out,
@@ -1820,7 +1841,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_de
 {
     k4_body<false>(comp, offsets, n, unit, hdr_mode, header_value, ring, allow_back, bias, out, status, blockIdx.x);
 }
+#endif
 
+#if SNAPPY_TU_DECODE
 __global__ __launch_bounds__(64) void k4_decompress_back(const uint8_t *__restrict__ comp,
                                                          const uint64_t *__restrict__ offsets, uint64_t n,
                                                          uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
@@ -1836,6 +1859,7 @@ __global__ __launch_bounds__(64) void k4_decompress_back(const uint8_t *__restri
     if (status[u] != SNAPPY_ST_DEFER) return;
     k4_body<true>(comp, offsets, n, unit, hdr_mode, header_value, ring, 1u, bias, out, status, u);
 }
+#endif
 // ---------------------------------------------------------------------------
 // K5: block index of a SINGLE-layout stream (one wave).  The stream is
 // walked through a 512-byte register window (two coalesced dword loads per
@@ -1851,6 +1875,7 @@ __device__ __forceinline__ uint32_t win_byte(uint32_t w0, uint32_t w1, uint32_t 
     return (v >> (8 * (rel & 3))) & 0xFF;
 }
 
+#if SNAPPY_TU_DECODE
 __global__ __launch_bounds__(64) void k5_index_stream(const uint8_t *__restrict__ comp, uint64_t clen,
                                                       uint64_t *__restrict__ offsets, uint64_t max_units,
                                                       int64_t *__restrict__ result)
@@ -1938,6 +1963,7 @@ __global__ __launch_bounds__(64) void k5_index_stream(const uint8_t *__restrict_
         result[2] = (int64_t)units;
     }
 }
+#endif
 
 
 // ---------------------------------------------------------------------------
@@ -1959,8 +1985,8 @@ __global__ __launch_bounds__(64) void k5_index_stream(const uint8_t *__restrict_
 //   K5d  first error in stream order, final offset.
 // Chunks entirely inside one element (long literals) are skipped.
 // ---------------------------------------------------------------------------
-constexpr uint32_t K5_S = 16384;
-constexpr uint64_t K5_SKIP = ~0ull;
+[[maybe_unused]] constexpr uint32_t K5_S = 16384;
+[[maybe_unused]] constexpr uint64_t K5_SKIP = ~0ull;
 
 struct K5Hdr {
     uint64_t N;
@@ -2026,6 +2052,7 @@ __device__ __forceinline__ bool k5_parse(const uint8_t *__restrict__ comp, uint6
     return x + hb <= clen;
 }
 
+#if SNAPPY_TU_DECODE
 __global__ __launch_bounds__(64) void k5a_chunk_walk(const uint8_t *__restrict__ comp, uint64_t clen,
                                                      uint64_t *__restrict__ X, uint64_t *__restrict__ O)
 {
@@ -2050,6 +2077,7 @@ __global__ __launch_bounds__(64) void k5a_chunk_walk(const uint8_t *__restrict__
     X[(uint64_t)c * 64 + lane] = x;
     O[(uint64_t)c * 64 + lane] = cum;
 }
+#endif
 
 // 64-bit readlane
 __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l)
@@ -2058,8 +2086,9 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l)
            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
 }
 
-constexpr uint32_t K5_G = 8;  // chunks per prefetch group
+[[maybe_unused]] constexpr uint32_t K5_G = 8;  // chunks per prefetch group
 
+#if SNAPPY_TU_DECODE
 __global__ __launch_bounds__(64) void k5b_carry(const uint8_t *__restrict__ comp, uint64_t clen, uint32_t nchunks,
                                                 const uint64_t *__restrict__ X, const uint64_t *__restrict__ O,
                                                 uint64_t *__restrict__ Ent, uint64_t *__restrict__ Base,
@@ -2126,7 +2155,9 @@ __global__ __launch_bounds__(64) void k5b_carry(const uint8_t *__restrict__ comp
         result[2] = (int64_t)base;  // output the chain accounts for (== N for a whole stream)
     }
 }
+#endif
 
+#if SNAPPY_TU_DECODE
 __global__ __launch_bounds__(64) void k5c_mark(const uint8_t *__restrict__ comp, uint64_t clen,
                                                const uint64_t *__restrict__ Ent, const uint64_t *__restrict__ Base,
                                                uint64_t *__restrict__ offsets, uint64_t max_units,
@@ -2179,7 +2210,9 @@ __global__ __launch_bounds__(64) void k5c_mark(const uint8_t *__restrict__ comp,
     }
     if (lane == 0) cst[c] = st;
 }
+#endif
 
+#if SNAPPY_TU_DECODE
 __global__ __launch_bounds__(64) void k5d_result(uint32_t nchunks, const int32_t *__restrict__ cst,
                                                  int64_t *__restrict__ result, uint64_t *__restrict__ offsets,
                                                  uint64_t max_units)
@@ -2201,10 +2234,11 @@ __global__ __launch_bounds__(64) void k5d_result(uint32_t nchunks, const int32_t
         result[2] = (int64_t)units;
     }
 }
+#endif
 
 }  // namespace snappy_amd
 
-#ifdef SNAPPY_K4_STATS
+#if defined(SNAPPY_K4_STATS) && SNAPPY_TU_DECODE
 extern "C" int snappy_amd_debug_k4_stats(uint64_t *host, size_t count)
 {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(snappy_amd::g_k4_stats), count * sizeof(uint64_t), 0,

@@ -116,7 +116,7 @@ def test_kernel_register_budget(tmp_path):
     import subprocess
     import sys
     llvm = "/opt/rocm/lib/llvm/bin"
-    obj = os.path.join(ROOT, "lightweight-snappy_amd", "build", "snappy_kernels.o")
+    obj = os.path.join(ROOT, "lightweight-snappy_amd", "build", "snappy_kernels_c.o")  # the compress kernels
     if not (os.path.exists(obj) and os.path.exists(f"{llvm}/llvm-objdump") and shutil.which("objcopy")):
         pytest.skip("needs the in-tree build object and the ROCm LLVM tools")
     fat, co = tmp_path / "fat.bin", tmp_path / "k.co"

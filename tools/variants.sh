@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 PKG=lightweight-snappy_amd
 mkdir -p $PKG/variants $PKG/build
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -Iinclude -I$PKG/csrc"
-KFLAGS="-mllvm -amdgpu-sched-strategy=max-ilp"  # as the Makefile
+KFLAGS=${KFLAGS-"-mllvm -amdgpu-sched-strategy=max-ilp"}  # as the Makefile (override: KFLAGS=...)
 hipcc $FLAGS -c $PKG/csrc/snappy_device.hip -o $PKG/build/dev_var.o
 gcc -O2 -fPIC -std=gnu11 -Iinclude -c $PKG/csrc/snappy_host.c -o $PKG/build/host_var.o
 for spec in "$@"; do

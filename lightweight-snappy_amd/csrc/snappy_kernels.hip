@@ -401,6 +401,12 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     // as soon as the ring moves, so the next advance finds it there instead of
     // waiting on a global load
     uint32_t seg_hi = kRegs;
+#ifdef SNAPPY_K1R_STATS
+    uint32_t n_farc = 0, n_reload = 0;  // BIG: candidate gathers from global memory, segments loaded synchronously
+#define K1R_COUNT(x) (x)++
+#else
+#define K1R_COUNT(x) do { } while (0)
+#endif
     __shared__ uint32_t ring_stage[64];
     uint32_t staged = 0;  // BIG: 1 + the segment in ring_stage, 0 = none
     auto stage = [&](uint32_t sg) {
@@ -439,7 +445,10 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 REG_SET_V(sg & (kRegs - 1), __builtin_bswap32(w));
                 sg++;
             }
-            for (; sg < need; sg++) REG_SET_V(sg & (kRegs - 1), load_word(sg));
+            for (; sg < need; sg++) {
+                K1R_COUNT(n_reload);
+                REG_SET_V(sg & (kRegs - 1), load_word(sg));
+            }
             seg_hi = need;
             if (decltype(pf)::value) stage(seg_hi);  // REG_SET_V consumed the LDS read: the DMA may overwrite it
         }
@@ -452,7 +461,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         uint32_t _cv;                                                                              \
         if constexpr (BIG) {                                                                       \
             if (__builtin_expect((_cd >> 6) + kRegs >= seg_hi, 1)) _cv = DW_LANES(_cd);             \
-            else _cv = load_dw(_cd + lane);                                                        \
+            else { K1R_COUNT(n_farc); _cv = load_dw(_cd + lane); }                                  \
         } else {                                                                                   \
             _cv = DW_LANES(_cd);                                                                   \
         }                                                                                          \
@@ -823,6 +832,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #undef TAG_EQ
 #undef LDS_ORDER
 #undef CAND_LANES
+#undef K1R_COUNT
     flush_tokens();
     // the tail literal is pseudo-token nt (src/snappy_compression.c:292-297)
     if (lane == 0) {
@@ -839,7 +849,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         st[3] = seg[2] | (seg[3] << 32);
         st[2] = seg[4] | (seg[5] << 32);
 #else
-        st[1] = 0;
+        st[1] = n_farc | ((uint64_t)n_reload << 32);
         st[2] = n_probe | ((uint64_t)n_round << 32);
         st[3] = n_match | ((uint64_t)n_refresh << 32);
 #endif

@@ -25,7 +25,7 @@ struct snappy_amd_ctx {
     size_t tokens_cap = 0;
     uint32_t *ntok = nullptr;
     size_t ntok_cap = 0;
-    uint32_t *seg_off = nullptr;    // K2 segment offsets inside each unit
+    uint32_t *seg_off = nullptr;    // K2 segments: (output offset in the unit, input position) pairs
     size_t seg_off_cap = 0;
     int32_t *status = nullptr;
     size_t status_cap = 0;
@@ -203,7 +203,7 @@ static int compress_impl(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t
     if ((rc = grow(reinterpret_cast<void **>(&c->sizes), &c->sizes_cap, units * sizeof(uint32_t)))) return rc;
     // segments per unit: tokens 0..ntok (the tail literal is token ntok <= tok_cap - 1)
     const uint32_t segs = (tok_cap + SNAPPY_K2_SEG - 1) / SNAPPY_K2_SEG;
-    if ((rc = grow(reinterpret_cast<void **>(&c->seg_off), &c->seg_off_cap, units * segs * sizeof(uint32_t))))
+    if ((rc = grow(reinterpret_cast<void **>(&c->seg_off), &c->seg_off_cap, units * segs * 2 * sizeof(uint32_t))))
         return rc;
     const uint32_t hm = hdr_mode_of(layout, flags);
     if (c->timing) (void)hipEventRecord(c->ev[0], c->stream);

@@ -478,11 +478,12 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     for (uint32_t i = lane; i < kTable; i += 64) TBL_WRITE(i, init);
     __syncthreads();
 
-    // tokens, structure of arrays (6 bytes each): position | length << 16 as
-    // u32, the copy offset (< 65,536) as u16 after all units' u32 words
+    // tokens, 4 bytes each: offset | (length - 4) << 16 | gap << 24, gap = the
+    // literal bytes before the copy; a length or gap that does not fit 8 bits
+    // (255 = escape) puts gap | length << 16 in the same slot of a second array
+    // (after all units' words), written only for those tokens
     uint32_t *tok = reinterpret_cast<uint32_t *>(tokens) + (uint64_t)u * tok_cap;
-    uint16_t *tok_off = reinterpret_cast<uint16_t *>(reinterpret_cast<uint32_t *>(tokens) +
-                                                     (uint64_t)gridDim.x * tok_cap) + (uint64_t)u * tok_cap;
+    uint32_t *tok_full = reinterpret_cast<uint32_t *>(tokens) + ((uint64_t)gridDim.x + u) * tok_cap;
     uint32_t tka = 0, tkb = 0;  // pending tokens: lane t < pend holds token nt + t
     uint32_t nt = 0, pend = 0;
     // encoded size so far (header, literals, copies: src/snappy_compression.c:95-165)
@@ -490,21 +491,25 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     uint32_t acc = 0, cend = 0;
     if (hdr_mode == SNAPPY_HDR_EVERY_UNIT) acc = varint_len(L);
     else if (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0) acc = varint_len(header_value);
-    uint32_t *const segu = seg_off + (uint64_t)u * segs;
+    // K2 segment k (tokens kK2Seg k ..): its output offset in the unit and the
+    // input position where its first token's literal starts
+    uint32_t *const segu = seg_off + 2 * (uint64_t)u * segs;
     auto flush_tokens = [&]() {
         const bool has = lane < pend;
-        if (has) {
-            tok[nt + lane] = tka;
-            tok_off[nt + lane] = (uint16_t)tkb;
-        }
         const uint32_t pos = tka & 0xFFFF, len = tka >> 16, end = pos + len;
         // lane l <- end of lane l - 1; lane 0 keeps cend (no bound_ctrl: the old value stays)
         const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp((int)cend, (int)end, 0x138, 0xF, 0xF, false);
         const uint32_t litn = pos - prev;
+        if (has) {
+            const uint32_t lc = len - 4 < 255 ? len - 4 : 255u, gc = litn < 255 ? litn : 255u;
+            tok[nt + lane] = tkb | (lc << 16) | (gc << 24);
+            if (lc == 255 || gc == 255) tok_full[nt + lane] = litn | (len << 16);
+        }
         const uint32_t b = has ? (litn ? literal_bytes(litn) : 0u) + copy_bytes(len, tkb) : 0u;
         uint32_t tot;
         const uint32_t ex = wave_excl_scan(b, lane, &tot);
-        if (has && ((nt + lane) & (kK2Seg - 1)) == 0) segu[(nt + lane) / kK2Seg] = acc + ex;
+        if (has && ((nt + lane) & (kK2Seg - 1)) == 0)
+            *reinterpret_cast<uint2 *>(segu + 2 * ((nt + lane) / kK2Seg)) = make_uint2(acc + ex, prev);
         if (pend) cend = __builtin_amdgcn_readlane(end, pend - 1);
         acc += tot;
         nt += pend;
@@ -836,7 +841,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     flush_tokens();
     // the tail literal is pseudo-token nt (src/snappy_compression.c:292-297)
     if (lane == 0) {
-        if ((nt & (kK2Seg - 1)) == 0) segu[nt / kK2Seg] = acc;
+        if ((nt & (kK2Seg - 1)) == 0) *reinterpret_cast<uint2 *>(segu + 2 * (nt / kK2Seg)) = make_uint2(acc, cend);
         ntok_out[u] = nt;
         sizes[u] = acc + (L > cend ? literal_bytes(L - cend) : 0u);
     }
@@ -1110,45 +1115,53 @@ __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(cons
     const uint32_t L = (uint32_t)((n - base) < unit ? (n - base) : unit);
     const uint8_t *src = in + base;
     uint8_t *dst = out + offsets[u];
+    // 4-byte tokens (K1r: offset | (length - 4) << 16 | gap << 24, escapes in tok_full)
     const uint32_t *tok = reinterpret_cast<const uint32_t *>(tokens) + (uint64_t)u * tok_cap;
-    const uint16_t *tok_off = reinterpret_cast<const uint16_t *>(reinterpret_cast<const uint32_t *>(tokens) +
-                                                                 (uint64_t)gridDim.x * tok_cap) + (uint64_t)u * tok_cap;
+    const uint32_t *tok_full = reinterpret_cast<const uint32_t *>(tokens) + ((uint64_t)gridDim.x + u) * tok_cap;
     if (blockIdx.y == 0) {
         if (hdr_mode == SNAPPY_HDR_EVERY_UNIT) varint_put(L, dst, lane);
         else if (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0) varint_put(header_value, dst, lane);
     }
     for (uint32_t sg = blockIdx.y; sg * kK2Seg <= nt; sg += gridDim.y) {
     const uint32_t c = sg * kK2Seg;
-    const uint32_t o = seg_off[(uint64_t)u * segs + sg];
-    // end of the previous segment's last token = start of this segment's first literal
-    uint32_t carry = 0;
-    if (c) {
-        const uint32_t k = tok[c - 1];
-        carry = (k & 0xFFFF) + (k >> 16);
-    }
+    // K1r's table: the segment's output offset and the input position where
+    // its first literal starts (the end of the previous segment's last token)
+    const uint2 se = *reinterpret_cast<const uint2 *>(seg_off + 2 * ((uint64_t)u * segs + sg));
+    const uint32_t o = se.x, carry = se.y;
 
-    uint32_t pos[kK2Per], len[kK2Per], off[kK2Per], pe[kK2Per], litn[kK2Per], hl[kK2Per], sz[kK2Per];
+    uint32_t gap[kK2Per], len[kK2Per], off[kK2Per], pe[kK2Per], litn[kK2Per], hl[kK2Per], sz[kK2Per];
     bool live[kK2Per];
+    uint32_t lspan = 0;  // input bytes covered by the lane's tokens (literal + copy)
 #pragma unroll
     for (uint32_t i = 0; i < kK2Per; i++) {
         const uint32_t t = c + kK2Per * lane + i;
-        pos[i] = L; len[i] = 0; off[i] = 0;  // pseudo-token: tail literal
+        gap[i] = 0; len[i] = 0; off[i] = 0;  // also the pseudo-token: the tail literal
         live[i] = t <= nt;
         if (t < nt) {
             const uint32_t k = tok[t];
-            pos[i] = k & 0xFFFF;
-            len[i] = k >> 16;
-            off[i] = tok_off[t];
-            if (len[i] == 0) len[i] = 65536;  // unreachable for units <= 32 KiB
+            const uint32_t lc = (k >> 16) & 0xFF, gc = k >> 24;
+            off[i] = k & 0xFFFF;
+            if (lc == 255 || gc == 255) {
+                const uint32_t f = tok_full[t];
+                gap[i] = f & 0xFFFF;
+                len[i] = f >> 16;
+            } else {
+                gap[i] = gc;
+                len[i] = lc + 4;
+            }
+            lspan += gap[i] + len[i];
         }
     }
-    uint32_t pe0 = (uint32_t)__shfl_up((int)(pos[kK2Per - 1] + len[kK2Per - 1]), 1, 64);
-    if (lane == 0) pe0 = carry;
+    uint32_t span_tot;
+    uint32_t cur = carry + wave_excl_scan(lspan, lane, &span_tot);
+    (void)span_tot;
     uint32_t lsum = 0;
 #pragma unroll
     for (uint32_t i = 0; i < kK2Per; i++) {
-        pe[i] = i ? pos[i - 1] + len[i - 1] : pe0;
-        litn[i] = live[i] ? pos[i] - pe[i] : 0;
+        const uint32_t t = c + kK2Per * lane + i;
+        pe[i] = cur;  // where the token's literal starts
+        litn[i] = t < nt ? gap[i] : (t == nt ? L - cur : 0u);
+        cur += gap[i] + len[i];
         hl[i] = litn[i] ? (litn[i] <= 60 ? 1 : (litn[i] <= 256 ? 2 : 3)) : 0;
         sz[i] = hl[i] + litn[i] + ((live[i] && len[i]) ? copy_bytes(len[i], off[i]) : 0);
         lsum += sz[i];

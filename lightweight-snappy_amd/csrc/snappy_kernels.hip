@@ -1732,7 +1732,11 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             const bool ex = lane < nexec;
             const uint32_t kop = e_op | (e_t == 0 ? 0x80000000u : 0u);
             const uint32_t kinfo = e_t == 0 ? e_lsrc : e_info;
-            for (uint32_t P = op; P < op_end; P += 64) {
+            // pass P, first half: which element each byte lane belongs to and
+            // everything that does not read the ring -- the byte's source
+            // position, or its value when it is a literal byte (register
+            // window) or a far copy byte (HBM); pw = value | direct << 8 | pend << 9
+            auto lookup = [&](uint32_t P, SrcT &src, uint32_t &pw) {
                 const uint32_t j = e_op - P;
                 const bool inw = ex && j < 64;
                 const uint32_t cb = (uint32_t)__builtin_popcountll(__ballot(ex && e_op < P));
@@ -1766,8 +1770,8 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                     const uint32_t qd = (uint32_t)((float)d * r + 0.0001f);
                     d -= qd * f_in;
                 }
-                const SrcT src = (SrcT)(f_op & 0x7FFFFFFFu) - (SrcT)f_in + (SrcT)d;
-                bool pend = o < op_end;
+                src = (SrcT)(f_op & 0x7FFFFFFFu) - (SrcT)f_in + (SrcT)d;
+                const bool pend = o < op_end;
                 if constexpr (BACK) {
                     // an overlapping copy near the unit start may repeat bytes of an earlier unit
                     if (!lit && pend && !farl && src < (SrcT)lo) {
@@ -1775,36 +1779,45 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                         farl = true;
                     }
                 }
+#ifdef SNAPPY_K4_STATS
+                n_far += __ballot(farl) != 0;
+#endif
+                pw = (uint32_t)(lit ? lb : fv) | ((lit || farl) ? 0x100u : 0u) | (pend ? 0x200u : 0u);
+            };
+            // pass P, second half: the ring
+            auto execute = [&](uint32_t P, SrcT src, uint32_t pw) {
+                const uint32_t o = P + lane;
+                const bool direct = (pw & 0x100u) != 0;
+                bool pend = (pw & 0x200u) != 0;
+#ifdef SNAPPY_K4_STATS
+                n_pass++;
+#endif
                 // the common pass: no byte depends on another byte of the same pass
-                if (!__ballot(pend && !lit && src >= (SrcT)P)) {
-                    if (pend) ob[o & M] = lit ? lb : (farl ? fv : ob[(uint32_t)src & M]);
+                if (!__ballot(pend && !direct && src >= (SrcT)P)) {
+                    if (pend) ob[o & M] = direct ? (uint8_t)pw : ob[(uint32_t)src & M];
 #ifdef SNAPPY_K4_STATS
                     n_sub++;
-                    n_pass++;
-                    n_far += __ballot(farl) != 0;
 #endif
-                    continue;
+                    return;
                 }
                 // else sub-passes: a byte is written once its source byte has been
                 uint64_t written = 0;
                 for (;;) {
-                    const bool rdy = pend && (lit || src < (SrcT)P || ((written >> ((uint32_t)(src - (SrcT)P) & 63)) & 1));
-                    if (rdy) {
-                        uint8_t v = lb;
-                        if (!lit) v = farl ? fv : ob[(uint32_t)src & M];
-                        ob[o & M] = v;
-                    }
+                    const bool rdy = pend && (direct || src < (SrcT)P || ((written >> ((uint32_t)(src - (SrcT)P) & 63)) & 1));
+                    if (rdy) ob[o & M] = direct ? (uint8_t)pw : ob[(uint32_t)src & M];
                     written |= __ballot(rdy);
                     pend = pend && !rdy;
 #ifdef SNAPPY_K4_STATS
                     n_sub++;
-                    n_far += __ballot(rdy && farl) != 0;
 #endif
                     if (!__ballot(pend)) break;
                 }
-#ifdef SNAPPY_K4_STATS
-                n_pass++;
-#endif
+            };
+            for (uint32_t P = op; P < op_end; P += 64) {
+                SrcT sa;
+                uint32_t wa;
+                lookup(P, sa, wa);
+                execute(P, sa, wa);
             }
         }
         K4STAMP(td);

@@ -40,8 +40,12 @@ __global__ void k2_emit_units(const uint8_t *__restrict__ in, uint64_t n, uint32
                               const uint32_t *__restrict__ ntok, const uint32_t *__restrict__ seg_off, uint32_t segs,
                               const uint64_t *__restrict__ offsets, uint8_t *__restrict__ out);
 // K2 segments: 256 tokens (4 per lane); waves per unit
+#ifndef SNAPPY_K2_SEG
 #define SNAPPY_K2_SEG 256u
+#endif
+#ifndef SNAPPY_K2_WAVES
 #define SNAPPY_K2_WAVES 8u
+#endif
 // register-resident K1r handles units up to this size (128 VGPRs x 64 lanes x 4 B)
 #define SNAPPY_K1R_MAX_UNIT 32768u
 

@@ -295,8 +295,16 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
 #endif
 
 // K2 segments: 4 consecutive tokens per lane, 256 per wave
-constexpr uint32_t kK2Per = 4;
-constexpr uint32_t kK2Seg = 64 * kK2Per;
+// K2 segments (K1r records each one's output offset and input position): 256
+// tokens; K2 walks a segment in passes of kK2Pass tokens, kK2Per per lane (2: 80
+// VGPRs, 6 waves per SIMD; a 256-token pass needs 114, 4 waves: 7 % slower)
+#ifndef SNAPPY_K2_PASS
+#define SNAPPY_K2_PASS 128u
+#endif
+constexpr uint32_t kK2Seg = SNAPPY_K2_SEG;
+constexpr uint32_t kK2Pass = SNAPPY_K2_PASS;
+constexpr uint32_t kK2Per = kK2Pass / 64;
+static_assert(kK2Pass % 64 == 0 && kK2Seg % kK2Pass == 0, "K2: passes of 64 k tokens dividing a segment");
 
 // Wave-wide inclusive add-scan in DPP (row_shr 1/2/4/8 inside 16-lane rows,
 // then row_bcast:15 / row_bcast:31 across rows): no LDS round trips.
@@ -971,10 +979,12 @@ constexpr uint32_t kK2Stage = SNAPPY_K2_STAGE;
 // put_element into the LDS stage without exec-mask branches: every store is
 // issued by every lane, lanes without a byte to store hit their own dummy
 // slot (stage + kK2Stage + 4 lane); full literal dwords as unaligned ds_write_b32
+// lw: the five source dwords of a short literal, loaded by the caller (all the
+// wave's literal loads in one round trip), sh = its source address & 3
 __device__ __forceinline__ void put_element_lds(__attribute__((address_space(3))) uint8_t *stage, uint32_t at,
                                                 const uint8_t *__restrict__ src, uint32_t s0, uint32_t litn,
                                                 uint32_t hl, uint32_t len, uint32_t off, bool wide_ok, bool live,
-                                                uint32_t lane)
+                                                uint32_t lane, const uint32_t *lw, uint32_t sh)
 {
     const uint32_t dum = kK2Stage + 4 * lane;
 #define K2_ST8(cond, adr, v) stage[(cond) ? (adr) : dum] = (uint8_t)(v)
@@ -986,12 +996,8 @@ __device__ __forceinline__ void put_element_lds(__attribute__((address_space(3))
     const uint32_t lp = at + hl;
     if (litn <= 16) {
         if (wide_ok) {
-            const uintptr_t sa = reinterpret_cast<uintptr_t>(src + s0);
-            const uint32_t sh = (uint32_t)(sa & 3);
-            const uint32_t *aw = reinterpret_cast<const uint32_t *>(sa - sh);
-            const uint32_t d0 = aw[0], d1 = aw[1], d2 = aw[2], d3 = aw[3], d4 = aw[4];
-            const uint32_t r0 = __builtin_amdgcn_alignbyte(d1, d0, sh), r1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-            const uint32_t r2 = __builtin_amdgcn_alignbyte(d3, d2, sh), r3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+            const uint32_t r0 = __builtin_amdgcn_alignbyte(lw[1], lw[0], sh), r1 = __builtin_amdgcn_alignbyte(lw[2], lw[1], sh);
+            const uint32_t r2 = __builtin_amdgcn_alignbyte(lw[3], lw[2], sh), r3 = __builtin_amdgcn_alignbyte(lw[4], lw[3], sh);
 #define K2_ST32(k, r) *(__attribute__((address_space(3))) u32u *)(stage + (live && 4 * (k) + 4 <= litn ? lp + 4 * (k) : dum)) = (r)
             K2_ST32(0, r0); K2_ST32(1, r1); K2_ST32(2, r2); K2_ST32(3, r3);
 #undef K2_ST32
@@ -1123,38 +1129,42 @@ __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(cons
         else if (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0) varint_put(header_value, dst, lane);
     }
     for (uint32_t sg = blockIdx.y; sg * kK2Seg <= nt; sg += gridDim.y) {
-    const uint32_t c = sg * kK2Seg;
     // K1r's table: the segment's output offset and the input position where
     // its first literal starts (the end of the previous segment's last token)
     const uint2 se = *reinterpret_cast<const uint2 *>(seg_off + 2 * ((uint64_t)u * segs + sg));
-    const uint32_t o = se.x, carry = se.y;
+    uint32_t o = se.x, carry = se.y;
+    for (uint32_t c = sg * kK2Seg; c < (sg + 1) * kK2Seg && c <= nt; c += kK2Pass) {
 
     uint32_t gap[kK2Per], len[kK2Per], off[kK2Per], pe[kK2Per], litn[kK2Per], hl[kK2Per], sz[kK2Per];
     bool live[kK2Per];
     uint32_t lspan = 0;  // input bytes covered by the lane's tokens (literal + copy)
+    // the lane's token words in one round trip (a lane past the end re-reads word 0:
+    // no branch, so no load waits for the one before it), then the rare escapes
+    uint32_t kw[kK2Per];
 #pragma unroll
     for (uint32_t i = 0; i < kK2Per; i++) {
         const uint32_t t = c + kK2Per * lane + i;
-        gap[i] = 0; len[i] = 0; off[i] = 0;  // also the pseudo-token: the tail literal
+        kw[i] = tok[t < nt ? t : 0u];
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kK2Per; i++) {
+        const uint32_t t = c + kK2Per * lane + i;
+        const bool has = t < nt;  // else the pseudo-token (the tail literal) or nothing
         live[i] = t <= nt;
-        if (t < nt) {
-            const uint32_t k = tok[t];
-            const uint32_t lc = (k >> 16) & 0xFF, gc = k >> 24;
-            off[i] = k & 0xFFFF;
-            if (lc == 255 || gc == 255) {
-                const uint32_t f = tok_full[t];
-                gap[i] = f & 0xFFFF;
-                len[i] = f >> 16;
-            } else {
-                gap[i] = gc;
-                len[i] = lc + 4;
-            }
-            lspan += gap[i] + len[i];
+        const uint32_t k = has ? kw[i] : 0xFFFFFFFFu;
+        const uint32_t lc = (k >> 16) & 0xFF, gc = k >> 24;
+        off[i] = has ? k & 0xFFFF : 0u;
+        gap[i] = has ? gc : 0u;
+        len[i] = has ? lc + 4 : 0u;
+        if (has && (lc == 255 || gc == 255)) {
+            const uint32_t f = tok_full[t];
+            gap[i] = f & 0xFFFF;
+            len[i] = f >> 16;
         }
+        lspan += gap[i] + len[i];
     }
     uint32_t span_tot;
     uint32_t cur = carry + wave_excl_scan(lspan, lane, &span_tot);
-    (void)span_tot;
     uint32_t lsum = 0;
 #pragma unroll
     for (uint32_t i = 0; i < kK2Per; i++) {
@@ -1171,10 +1181,26 @@ __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(cons
     const bool staged = total <= kK2Stage;
     uint64_t longs[kK2Per];
     uint32_t d0v[kK2Per];
+    // every short literal's source dwords in one round trip: lanes with none read
+    // the unit's first token words (in bounds, ignored)
+    uint32_t lw[kK2Per][5], lsh[kK2Per];
+    bool wide[kK2Per];
 #pragma unroll
     for (uint32_t i = 0; i < kK2Per; i++) {
-        const bool wide_ok = base + pe[i] + 20 <= n;  // the aligned 20-byte read ends inside in[0, n)
-        if (staged) put_element_lds(stage, rel, src, pe[i], litn[i], hl[i], len[i], off[i], wide_ok, live[i], lane);
+        wide[i] = base + pe[i] + 20 <= n;  // the aligned 20-byte read ends inside in[0, n)
+        const bool ld = staged && wide[i] && live[i] && litn[i] != 0 && litn[i] <= 16;
+        const uintptr_t sa = reinterpret_cast<uintptr_t>(src + pe[i]);
+        lsh[i] = (uint32_t)(sa & 3);
+        const auto *aw = reinterpret_cast<const __attribute__((address_space(1))) uint32_t *>(
+            ld ? sa - lsh[i] : reinterpret_cast<uintptr_t>(tok));
+#pragma unroll
+        for (uint32_t j = 0; j < 5; j++) lw[i][j] = aw[j];
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kK2Per; i++) {
+        const bool wide_ok = wide[i];
+        if (staged) put_element_lds(stage, rel, src, pe[i], litn[i], hl[i], len[i], off[i], wide_ok, live[i], lane,
+                                    lw[i], lsh[i]);
         else if (live[i]) put_element(dst + o + rel, src, pe[i], litn[i], hl[i], len[i], off[i], wide_ok);
         longs[i] = __ballot(live[i] && litn[i] > 16);
         d0v[i] = rel + hl[i];
@@ -1199,7 +1225,10 @@ __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(cons
         const uint32_t tail0 = head + 4 * nw;
         if (lane < total - tail0) g[tail0 + lane] = stage[tail0 + lane];
     }
-    __builtin_amdgcn_wave_barrier();  // the stage is reused by the next segment
+    __builtin_amdgcn_wave_barrier();  // the stage is reused by the next pass
+    o += total;
+    carry += span_tot;
+    }
     }
 }
 #endif

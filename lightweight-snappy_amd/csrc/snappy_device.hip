@@ -456,6 +456,18 @@ size_t read_full(FILE *f, uint8_t *b, size_t cap)
     return n;
 }
 
+void slot_free(StreamSlot &s)
+{
+    for (void *h : {(void *)s.h_in, (void *)s.h_out, (void *)s.h_idx})
+        if (h) (void)hipHostFree(h);
+    for (void *d : {(void *)s.d_in, (void *)s.d_out, (void *)s.d_idx})
+        if (d) (void)hipFree(d);
+    snappy_amd_destroy(s.c);
+    s = StreamSlot{};
+}
+
+// a slot is usable only when every buffer exists: a partial failure frees
+// what was allocated, so the next call retries from scratch
 int slot_init(StreamSlot &s, int device)
 {
     if (s.c) return SNAPPY_AMD_OK;
@@ -467,8 +479,10 @@ int slot_init(StreamSlot &s, int device)
         hipHostMalloc(&s.h_out, maxo, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&s.h_idx, (units + 1) * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
         hipMalloc(&s.d_in, kStreamChunk) != hipSuccess || hipMalloc(&s.d_out, maxo) != hipSuccess ||
-        hipMalloc(&s.d_idx, (units + 1) * sizeof(uint64_t)) != hipSuccess)
+        hipMalloc(&s.d_idx, (units + 1) * sizeof(uint64_t)) != hipSuccess) {
+        slot_free(s);
         return SNAPPY_AMD_ERR_DEVICE;
+    }
     return SNAPPY_AMD_OK;
 }
 

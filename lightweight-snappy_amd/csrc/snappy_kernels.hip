@@ -97,7 +97,9 @@ __device__ __forceinline__ uint32_t skipsum(uint32_t m)
 //    length found by 16 lanes comparing 64 bytes per step.
 //  * Larger steps (skip >= 61, incompressible data) use W = 4 speculative
 //    probes at their closed-form positions with explicit conflict stops.
-//  * Output is a token list (pos | len << 16, offset); K2s sizes it, K3 places
+//  * Output is a token list (4 bytes each: offset | (length - 4) << 16 |
+//    literal gap << 24, escapes in a second array), the unit's exact encoded
+//    size and every 256th token's output offset / input position; K3 places
 //    every unit, K2 writes the bytes.
 // 12 KiB LDS and <= 168 VGPRs -> 12 units per CU (3 waves per SIMD), both
 // kernels.
@@ -294,7 +296,6 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
 #define LSEG(i, a, b) do { } while (0)
 #endif
 
-// K2 segments: 4 consecutive tokens per lane, 256 per wave
 // K2 segments (K1r records each one's output offset and input position): 256
 // tokens; K2 walks a segment in passes of kK2Pass tokens, kK2Per per lane (2: 80
 // VGPRs, 6 waves per SIMD; a 256-token pass needs 114, 4 waves: 7 % slower)
@@ -964,12 +965,13 @@ __device__ __forceinline__ void put_element(P *w, const uint8_t *__restrict__ sr
 }
 
 // K2: tokens -> bytes at the unit's final offset (write_literal :95-120,
-// write_copy :153-165).  One wave per (unit, segment of kK2Seg tokens, 4
-// consecutive per lane): each wave makes a single pass with two memory round
-// trips (tokens, then literal bytes), so the latency of one unit's passes is
-// spread over many waves.  The pass is assembled in LDS (byte writes are cheap
-// there) and leaves as aligned dword stores; larger passes (long copies /
-// literals) write HBM directly.
+// write_copy :153-165).  gridDim.y waves per unit, wave y taking segments y,
+// y + gridDim.y, ... of kK2Seg tokens (K1r recorded each segment's output
+// offset and input position, so segments are independent), each segment in
+// passes of kK2Pass tokens (kK2Per consecutive per lane) with two memory round
+// trips (the token words, then every short literal's source dwords).  The
+// pass is assembled in LDS (byte writes are cheap there) and leaves as aligned
+// dword stores; larger passes (long copies / literals) write HBM directly.
 // 4 KiB holds a text segment (~2 KiB of output) and keeps K2 at 32 waves per CU
 #ifndef SNAPPY_K2_STAGE
 #define SNAPPY_K2_STAGE 4096
@@ -1099,8 +1101,9 @@ __device__ __forceinline__ void k2_long_literals(uint8_t *w, const uint8_t *__re
     }
 }
 
-// 1: no register cap (88 VGPRs, 5 waves/SIMD); 6 or 8 waves spill to scratch and
-// measured no better (tools/variant_bench.py, 256 MiB text: 0.295 / 0.294 / 0.325 ms)
+// 1: no register cap (80 VGPRs, 6 waves/SIMD with 128-token passes); capping at
+// 7 or 8 waves spills and measured slower (1.18 / 1.22 against 0.979
+// ms of K3 + K2 per GiB of text)
 #ifndef SNAPPY_K2_WAVES_PER_EU
 #define SNAPPY_K2_WAVES_PER_EU 1
 #endif

@@ -229,6 +229,27 @@ def test_parallel_index_matches_serial_and_compressor(codec):
         assert np.array_equal(o1, want) and np.array_equal(o2, want)
 
 
+def test_parallel_index_chains_that_never_converge(codec):
+    """K5a's per-lane fallback: a stream of 2-byte copy-1 elements (01 01: length 4,
+    offset 1) parses as a valid element at EVERY byte, so the chains entered at even
+    and odd bytes of a chunk never meet; likewise 3-byte copy-2 elements whose
+    offset bytes are again valid copy-2 tags (period 3).  Index = serial walk, and
+    the decode equals the oracle's."""
+    import torch
+    lit = bytes(range(200)) * 3  # 600-byte literal: tag 61 << 2, length - 1 in 2 bytes
+    for unit, elen, count in (((1, 1), 4, 3_000_000), ((2, 2, 2), 1, 2_000_000)):
+        # 01 01: copy-1, length 4, offset 1; 02 02 02: copy-2, length 1, offset 514
+        n = len(lit) + elen * count
+        stream = snappy_amd.varint_encode(n) + bytes([61 << 2, 599 & 0xFF, 599 >> 8]) + lit + bytes(unit) * count
+        want = oracle.decompress(stream)
+        assert len(want) == n
+        d = torch.from_numpy(np.frombuffer(stream, dtype=np.uint8).copy()).cuda()
+        (c1, n1, o1), (c2, n2, o2) = _index_both(codec, d)
+        assert c1 == c2 == 0 and n1 == n2 == n and np.array_equal(o1, o2)
+        back = codec.decompress_tensor(d, torch.from_numpy(o1).cuda(), n1, layout=snappy_amd.SINGLE)
+        assert back.cpu().numpy().tobytes() == want
+
+
 def test_parallel_index_errors_match_serial(codec):
     import torch
     a = datagen.make("T", 6 << 20, 33)

@@ -2038,18 +2038,20 @@ __global__ __launch_bounds__(64) void k5_index_stream(const uint8_t *__restrict_
 // K5p: block index of a foreign SINGLE stream, chunk-parallel.  A stream has
 // no block markers (the decoder of src/snappy_decompression.c:345-363 just
 // walks elements until 65,536 bytes came out), so the walk is split into
-// K5_S-byte chunks of compressed stream:
-//   K5a  every chunk walks speculatively from its first byte, keeping the
-//        first 64 element starts it visits (with the output before each),
-//        its exit (first start at or past the chunk end) and its output;
-//   K5b1 chunk c checks whether the exit of chunk c-1 is one of its visited
-//        starts (element chains through the same bytes coincide from the
-//        first common start on);
-//   K5b2 one wave carries the true entry and output base through the chunks
-//        (hypothesis hits cost a few SALU ops, misses walk serially);
-//   K5c  every chunk re-walks from its true entry with the true output base
-//        and records the element starts where the output reaches a multiple
-//        of 65,536 (with the checks of K5);
+// K5_S-byte chunks of compressed stream, each staged in LDS (chunk + halo):
+//   K5a  lane l walks the element chain entered at byte l of its chunk to the
+//        chunk end: its exit (first start at or past the end) and output.
+//        The 64 chains walk element by element to a checkpoint; chains through
+//        a common start coincide from there on, so when every unfinished lane
+//        stands on one start (text: always) the rest is ONE chain, walked by
+//        batch parse (every byte of a 64-byte window parsed as a candidate
+//        element, the chain found by pointer doubling over ds_bpermute, sizes
+//        and outputs by DPP scans); otherwise every lane walks on alone;
+//   K5b  one wave carries the true entry and output base through the chunks
+//        (an entry < 64 bytes in is a K5a lookup, a later one walks);
+//   K5c  every chunk re-walks its true chain from the true entry with the true
+//        output base by batch parse and records the element holding each
+//        multiple of 65,536 (with the checks of K5);
 //   K5d  first error in stream order, final offset.
 // Chunks entirely inside one element (long literals) are skipped.
 // ---------------------------------------------------------------------------
@@ -2120,33 +2122,6 @@ __device__ __forceinline__ bool k5_parse(const uint8_t *__restrict__ comp, uint6
     return x + hb <= clen;
 }
 
-#if SNAPPY_TU_DECODE
-__global__ __launch_bounds__(64) void k5a_chunk_walk(const uint8_t *__restrict__ comp, uint64_t clen,
-                                                     uint64_t *__restrict__ X, uint64_t *__restrict__ O)
-{
-    // lane l walks from byte l of the chunk: every entry offset < 64 is
-    // covered exactly (no reliance on chains converging; a periodic stream
-    // never re-synchronises)
-    const uint32_t lane = threadIdx.x;
-    const uint32_t c = blockIdx.x;
-    const K5Hdr h = k5_header(comp, clen);
-    const uint64_t c0 = h.len + (uint64_t)c * K5_S;
-    const uint64_t end = c0 + K5_S < clen ? c0 + K5_S : clen;
-    uint64_t x = c0 + lane, cum = 0;
-    while (x < end) {
-        uint64_t size, len;
-        if (!k5_parse(comp, clen, x, size, len)) {
-            x = clen + 1;
-            break;
-        }
-        cum += len;
-        x += size;
-    }
-    X[(uint64_t)c * 64 + lane] = x;
-    O[(uint64_t)c * 64 + lane] = cum;
-}
-#endif
-
 // 64-bit readlane
 __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l)
 {
@@ -2154,7 +2129,222 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l)
            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
 }
 
-[[maybe_unused]] constexpr uint32_t K5_G = 8;  // chunks per prefetch group
+// LDS image of a chunk: the dwords from c0 & ~3 on, K5_S + 128 bytes (a batch
+// window starting before the chunk end reads at most 76 bytes past it), zero
+// at and past clen.  Byte r of the chunk (r relative to c0) is image byte r + o0.
+constexpr uint32_t K5_IMG = K5_S + 128;
+
+__device__ __forceinline__ void k5_stage(const uint8_t *__restrict__ comp, uint64_t clen, uint64_t c0, uint32_t *img,
+                                         uint32_t lane)
+{
+    const uint64_t a0 = c0 & ~3ull;
+    uint32_t v[8];
+    for (uint32_t i0 = 0; i0 < K5_IMG / 4; i0 += 8 * 64) {
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {  // 8 loads per lane in flight
+            const uint32_t i = i0 + 64 * j + lane;
+            v[j] = i < K5_IMG / 4 ? load_dw_guarded(comp, a0 + 4ull * i, clen) : 0u;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            const uint32_t i = i0 + 64 * j + lane;
+            if (i < K5_IMG / 4) img[i] = v[j];
+        }
+    }
+    __syncthreads();
+}
+
+// the element at image byte q (rem = stream bytes from it to clen): as k5_parse
+__device__ __forceinline__ bool k5_parse_img(const uint32_t *img, uint32_t q, uint64_t rem, uint64_t &size,
+                                             uint64_t &len)
+{
+    const uint32_t a = q >> 2, sh = 8 * (q & 3);
+    const uint32_t d0 = img[a], d1 = img[a + 1];
+    const uint32_t x0 = sh ? (d0 >> sh) | (d1 << (32 - sh)) : d0;  // bytes 0..3
+    const uint32_t b4 = (d1 >> sh) & 0xFF;                        // byte 4
+    const uint32_t tag = x0 & 0xFF, t = tag & 3, m = tag >> 2;
+    uint32_t hb;
+    if (t == 0) {
+        const uint32_t k = m >= 60 ? m - 59 : 0;
+        const uint32_t lv = k == 0 ? m : (k == 4 ? (x0 >> 8) | (b4 << 24) : (x0 >> 8) & ((1u << (8 * k)) - 1));
+        len = (uint64_t)lv + 1;
+        hb = 1 + k;
+        size = hb + len;
+    } else {
+        len = t == 1 ? (m & 7) + 4 : m + 1;
+        hb = t == 1 ? 2 : (t == 2 ? 3 : 5);
+        size = hb;
+    }
+    return rem > 0 && hb <= rem;
+}
+
+// Walk ONE element chain (x uniform, relative to c0) while x < end_rel (and,
+// MARK, op < N) by batch parse.  Not MARK (K5a): op accumulates the output, a
+// header past clen ends the walk with x = clen + 1 - c0.  MARK (K5c): op is
+// the absolute output position; the checks and index entries of the serial
+// walk (an element holding a multiple of 65,536 strictly inside it gets a
+// straddle entry, one ending on it the entry of its successor); any error
+// leaves st set (the index is then discarded, so extra entries are harmless).
+template <bool MARK>
+__device__ __forceinline__ void k5_chain(const uint32_t *img, uint32_t o0, uint64_t c0, uint64_t clen, uint32_t end_rel,
+                                         uint64_t &x, uint64_t &op, uint64_t N, uint64_t *__restrict__ offsets,
+                                         uint64_t max_units, int32_t &st, uint32_t lane)
+{
+    while (x < end_rel && (!MARK || op < N) && st == SNAPPY_ST_OK) {
+        const uint32_t r = (uint32_t)x + lane;
+        uint64_t size, len;
+        const bool ok = k5_parse_img(img, r + o0, c0 + r < clen ? clen - (c0 + r) : 0, size, len);
+        // element chain from lane 0 by pointer doubling: lane k <- start of element k
+        const uint32_t nx = lane + (size < 64 ? (uint32_t)size : 64u);
+#define K5JUMP(T, idx) ({ const uint32_t _i = (idx);                                                  \
+        const uint32_t _g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_i & 63) << 2), (int)(T));    \
+        _i < 64 ? _g : _i; })
+        const uint32_t J1 = nx, J2 = K5JUMP(J1, J1), J4 = K5JUMP(J2, J2), J8 = K5JUMP(J4, J4), J16 = K5JUMP(J8, J8);
+        uint32_t pos = 0;
+        { const uint32_t g = K5JUMP(J1, pos); pos = (lane & 1) ? g : pos; }
+        { const uint32_t g = K5JUMP(J2, pos); pos = (lane & 2) ? g : pos; }
+        { const uint32_t g = K5JUMP(J4, pos); pos = (lane & 4) ? g : pos; }
+        { const uint32_t g = K5JUMP(J8, pos); pos = (lane & 8) ? g : pos; }
+        { const uint32_t g = K5JUMP(J16, pos); pos = (lane & 16) ? g : pos; }
+#undef K5JUMP
+        // elements of at least 2 bytes: <= 32 start in the window; only starts before the chunk end count
+        const bool in = lane < 32 && pos < 64 && (uint32_t)x + pos < end_rel;
+        const uint32_t E = (uint32_t)__builtin_popcountll(__ballot(in));  // lanes 0..E-1 (>= 1: lane 0 is x)
+        const uint32_t pg = (in ? pos : 0u) << 2;
+        const uint32_t s_lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)pg, (int)(uint32_t)size);
+        const uint32_t s_hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)pg, (int)((uint32_t)(size >> 32) | (ok ? 0u : 0x80000000u)));
+        const uint32_t l_lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)pg, (int)(uint32_t)len);
+        const uint32_t l_hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)pg, (int)(uint32_t)(len >> 32));
+        const bool live = lane < E;
+        const bool e_ok = (s_hi >> 31) == 0;
+        const uint64_t e_size = ((uint64_t)(s_hi & 0x7FFFFFFFu) << 32) | s_lo;
+        const uint64_t e_len = ((uint64_t)l_hi << 32) | l_lo;
+        // exclusive prefix sums (64-bit values < 2^33, as 16-bit low parts + the rest)
+        uint32_t t0, t1, t2, t3;
+        const uint32_t sl = wave_excl_scan32(live ? (uint32_t)e_size & 0xFFFF : 0u, &t0);
+        const uint32_t sh = wave_excl_scan32(live ? (uint32_t)(e_size >> 16) : 0u, &t1);
+        const uint32_t ll = wave_excl_scan32(live ? (uint32_t)e_len & 0xFFFF : 0u, &t2);
+        const uint32_t lh = wave_excl_scan32(live ? (uint32_t)(e_len >> 16) : 0u, &t3);
+        const uint64_t e_x = x + ((uint64_t)sh << 16) + sl;  // relative start
+        const uint64_t e_op = op + ((uint64_t)lh << 16) + ll;
+        // the first element that ends the walk: a bad header (both), a truncated
+        // element (MARK), or (MARK) one at or past N (not run) / past N (run, then OVERRUN)
+        bool bad = !e_ok, skipn = false, over = false;
+        if constexpr (MARK) {
+            bad = bad || c0 + e_x + e_size > clen;
+            skipn = e_op >= N;
+            over = e_op + e_len > N;
+        }
+        const uint64_t stopm = __ballot(live && (bad || skipn || over));
+        uint32_t nexec = E;
+        int32_t er = SNAPPY_ST_OK;
+        if (stopm) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(stopm);
+            const uint32_t kb = __builtin_amdgcn_readlane((uint32_t)bad, k), ks = __builtin_amdgcn_readlane((uint32_t)skipn, k);
+            if (kb) {
+                nexec = k;
+                er = SNAPPY_ST_TRUNCATED;
+            } else if (ks) {
+                nexec = k;
+            } else {
+                nexec = k + 1;
+                er = SNAPPY_ST_OVERRUN;
+            }
+        }
+        if constexpr (MARK) {
+            const bool run = lane < nexec;
+            const uint64_t e_end = e_op + e_len;
+            // an element ending on a block boundary: the next entry is its successor
+            if (run && (e_end & (SNAPPY_BLOCK - 1)) == 0 && e_end < N) {
+                const uint64_t uu = e_end / SNAPPY_BLOCK;
+                if (uu < max_units) offsets[uu] = c0 + e_x + e_size;
+            }
+            // boundaries strictly inside an element (rare: serial over those lanes)
+            const uint64_t nb1 = (e_op / SNAPPY_BLOCK + 1) * SNAPPY_BLOCK;
+            uint64_t sm = __ballot(run && nb1 < e_end && nb1 < N);
+            while (sm) {
+                const uint32_t k = (uint32_t)__builtin_ctzll(sm);
+                sm &= sm - 1;
+                const uint64_t kop = rl64(e_op, k), kend = rl64(e_end, k), kx = c0 + rl64(e_x, k);
+                for (uint64_t nb = (kop / SNAPPY_BLOCK + 1) * SNAPPY_BLOCK; nb < kend && nb < N; nb += SNAPPY_BLOCK) {
+                    const uint64_t skip = nb - kop;
+                    if ((skip >> 24) || (kx >> 40)) {
+                        er = SNAPPY_ST_UNSUPPORTED;
+                        break;
+                    }
+                    const uint64_t uu = nb / SNAPPY_BLOCK;
+                    if (lane == 0 && uu < max_units) offsets[uu] = kx | (skip << 40);
+                }
+            }
+        }
+        if (nexec) {
+            x = rl64(e_x, nexec - 1) + rl64(e_size, nexec - 1);
+            op = rl64(e_op, nexec - 1) + rl64(e_len, nexec - 1);
+        }
+        if (er != SNAPPY_ST_OK) {
+            if constexpr (MARK) st = er;
+            else x = clen + 1 - c0;  // a header past clen (the only error without MARK)
+        }
+    }
+}
+
+#if SNAPPY_TU_DECODE
+__global__ __launch_bounds__(64) void k5a_chunk_walk(const uint8_t *__restrict__ comp, uint64_t clen,
+                                                     uint64_t *__restrict__ X, uint64_t *__restrict__ O)
+{
+    // lane l: the chain entered at byte l of the chunk (every entry offset < 64
+    // covered exactly; chains need not converge -- a periodic stream never
+    // re-synchronises, and then every lane walks alone)
+    __shared__ uint32_t img[K5_IMG / 4 + 4];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t c = blockIdx.x;
+    const K5Hdr h = k5_header(comp, clen);
+    const uint64_t c0 = h.len + (uint64_t)c * K5_S;
+    const uint32_t end_rel = (uint32_t)(c0 + K5_S < clen ? K5_S : clen - c0);
+    const uint32_t o0 = (uint32_t)(c0 & 3);
+    k5_stage(comp, clen, c0, img, lane);
+    uint64_t x = lane, cum = 0;
+    // element by element to the checkpoint (or the end), then alone if the chains differ
+    auto walk_to = [&](uint32_t lim) {
+        while (__ballot(x < lim)) {
+            if (x < lim) {
+                uint64_t size, len;
+                const uint32_t r = (uint32_t)x;
+                if (!k5_parse_img(img, r + o0, c0 + r < clen ? clen - (c0 + r) : 0, size, len)) {
+                    x = clen + 1 - c0;
+                } else {
+                    cum += len;
+                    x += size;
+                }
+            }
+        }
+    };
+    constexpr uint32_t kCheck = 192;
+    walk_to(end_rel < kCheck ? end_rel : kCheck);
+    const uint64_t open = __ballot(x < end_rel);
+    if (open) {
+        const uint32_t x1 = __builtin_amdgcn_readlane((uint32_t)x, (uint32_t)__builtin_ctzll(open));
+        if (!__ballot(x < end_rel && (uint32_t)x != x1)) {
+            uint64_t xe = x1, oe = 0;
+            int32_t st = SNAPPY_ST_OK;
+            k5_chain<false>(img, o0, c0, clen, end_rel, xe, oe, 0, nullptr, 0, st, lane);
+            if (x < end_rel) {
+                x = xe;
+                cum += oe;
+            }
+        } else {
+            walk_to(end_rel);
+        }
+    }
+    X[(uint64_t)c * 64 + lane] = c0 + x;
+    O[(uint64_t)c * 64 + lane] = cum;
+}
+#endif
+
+#ifndef SNAPPY_K5_G
+#define SNAPPY_K5_G 8
+#endif
+[[maybe_unused]] constexpr uint32_t K5_G = SNAPPY_K5_G;  // chunks per prefetch group
 
 #if SNAPPY_TU_DECODE
 __global__ __launch_bounds__(64) void k5b_carry(const uint8_t *__restrict__ comp, uint64_t clen, uint32_t nchunks,
@@ -2231,6 +2421,7 @@ __global__ __launch_bounds__(64) void k5c_mark(const uint8_t *__restrict__ comp,
                                                uint64_t *__restrict__ offsets, uint64_t max_units,
                                                int32_t *__restrict__ cst, uint64_t *__restrict__ fin)
 {
+    __shared__ uint32_t img[K5_IMG / 4 + 4];
     const uint32_t lane = threadIdx.x;
     const uint32_t c = blockIdx.x;
     const K5Hdr h = k5_header(comp, clen);
@@ -2240,36 +2431,11 @@ __global__ __launch_bounds__(64) void k5c_mark(const uint8_t *__restrict__ comp,
         const uint64_t N = h.N;
         const uint64_t units = (N + SNAPPY_BLOCK - 1) / SNAPPY_BLOCK;
         const uint64_t c0 = h.len + (uint64_t)c * K5_S;
-        const uint64_t end = c0 + K5_S < clen ? c0 + K5_S : clen;
-        uint64_t op = Base[c];
-        while (x < end && op < N) {
-            uint64_t size, len;
-            if (!k5_parse(comp, clen, x, size, len) || x + size > clen) {
-                st = SNAPPY_ST_TRUNCATED;
-                break;
-            }
-            // boundaries strictly inside the element: straddle entries
-            for (uint64_t nb = (op / SNAPPY_BLOCK + 1) * SNAPPY_BLOCK; nb < op + len && nb < N; nb += SNAPPY_BLOCK) {
-                const uint64_t skip = nb - op;
-                if ((skip >> 24) || (x >> 40)) {
-                    st = SNAPPY_ST_UNSUPPORTED;
-                    break;
-                }
-                const uint64_t u = nb / SNAPPY_BLOCK;
-                if (lane == 0 && u < max_units) offsets[u] = x | (skip << 40);
-            }
-            if (st != SNAPPY_ST_OK) break;
-            op += len;
-            x += size;
-            if (op > N) {
-                st = SNAPPY_ST_OVERRUN;
-                break;
-            }
-            if ((op & (SNAPPY_BLOCK - 1)) == 0 && op < N && lane == 0) {
-                const uint64_t u = op / SNAPPY_BLOCK;
-                if (u < max_units) offsets[u] = x;
-            }
-        }
+        const uint32_t end_rel = (uint32_t)(c0 + K5_S < clen ? K5_S : clen - c0);
+        k5_stage(comp, clen, c0, img, lane);
+        uint64_t op = Base[c], xr = x - c0;
+        k5_chain<true>(img, (uint32_t)(c0 & 3), c0, clen, end_rel, xr, op, N, offsets, max_units, st, lane);
+        x = c0 + xr;
         if (st == SNAPPY_ST_OK && op == N && lane == 0) {
             if (units < max_units) offsets[units] = x;
             *fin = x;

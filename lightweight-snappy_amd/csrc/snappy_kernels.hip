@@ -2319,10 +2319,13 @@ __global__ __launch_bounds__(64) void k5a_chunk_walk(const uint8_t *__restrict__
             }
         }
     };
+    // checkpoints every kCheck bytes: as soon as the unfinished lanes stand on
+    // one start, the rest is one batch-parsed chain
     constexpr uint32_t kCheck = 192;
-    walk_to(end_rel < kCheck ? end_rel : kCheck);
-    const uint64_t open = __ballot(x < end_rel);
-    if (open) {
+    for (uint32_t lim = kCheck;; lim += kCheck) {
+        walk_to(end_rel < lim ? end_rel : lim);
+        const uint64_t open = __ballot(x < end_rel);
+        if (!open) break;
         const uint32_t x1 = __builtin_amdgcn_readlane((uint32_t)x, (uint32_t)__builtin_ctzll(open));
         if (!__ballot(x < end_rel && (uint32_t)x != x1)) {
             uint64_t xe = x1, oe = 0;
@@ -2332,8 +2335,7 @@ __global__ __launch_bounds__(64) void k5a_chunk_walk(const uint8_t *__restrict__
                 x = xe;
                 cum += oe;
             }
-        } else {
-            walk_to(end_rel);
+            break;
         }
     }
     X[(uint64_t)c * 64 + lane] = c0 + x;

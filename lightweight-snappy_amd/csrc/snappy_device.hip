@@ -357,15 +357,23 @@ int snappy_amd_index_device(snappy_amd_ctx *c, const void *d_comp, size_t clen, 
     } else {
         // chunk-parallel walk (K5a..K5d); chunk c covers [hdr + c*K5_CHUNK, +K5_CHUNK)
         const uint32_t nch = (uint32_t)((clen + K5_CHUNK - 1) / K5_CHUNK);
-        const size_t per = 2 * 64 * 8 + 2 * 8 + 4;
-        int rc = grow(reinterpret_cast<void **>(&c->k5buf), &c->k5buf_cap, per * nch + 64);
+        // per chunk: X, O (u64 x 64), P (u32 x 64), Ent, Base, status; per 64-chunk
+        // block: F (u64 x 64), BE, BB
+        const uint32_t nblk = (nch + 63) / 64;
+        const size_t per = 2 * 64 * 8 + 64 * 4 + 2 * 8 + 4;
+        int rc = grow(reinterpret_cast<void **>(&c->k5buf), &c->k5buf_cap, per * nch + (64 * 8 + 16) * (size_t)nblk + 128);
         if (rc) return rc;
         uint64_t *X = reinterpret_cast<uint64_t *>(c->k5buf);
         uint64_t *O = X + 64 * (size_t)nch, *Ent = O + 64 * (size_t)nch, *Base = Ent + nch, *fin = Base + nch;
-        int32_t *cst = reinterpret_cast<int32_t *>(fin + 8);
-        hipLaunchKernelGGL(k5a_chunk_walk, dim3(nch), dim3(64), 0, c->stream, comp, (uint64_t)clen, X, O);
-        hipLaunchKernelGGL(k5b_carry, dim3(1), dim3(64), 0, c->stream, comp, (uint64_t)clen, nch, X, O, Ent, Base,
-                           c->k5res);
+        uint64_t *F = fin + 8, *BE = F + 64 * (size_t)nblk, *BB = BE + nblk;
+        int32_t *cst = reinterpret_cast<int32_t *>(BB + nblk);
+        uint32_t *P = reinterpret_cast<uint32_t *>(cst + nch);
+        hipLaunchKernelGGL(k5a_chunk_walk, dim3(nch), dim3(64), 0, c->stream, comp, (uint64_t)clen, X, O, P);
+        hipLaunchKernelGGL(k5b1_compose, dim3(nblk), dim3(64), 0, c->stream, (const uint32_t *)P, nch, F);
+        hipLaunchKernelGGL(k5b_carry, dim3(1), dim3(64), 0, c->stream, comp, (uint64_t)clen, nch, X, O,
+                           (const uint64_t *)F, BE, BB, Ent, Base, c->k5res);
+        hipLaunchKernelGGL(k5b3_fill, dim3(nblk), dim3(64), 0, c->stream, comp, (uint64_t)clen, (const uint32_t *)P,
+                           nch, (const uint64_t *)BE, (const uint64_t *)BB, Ent, Base);
         hipLaunchKernelGGL(k5c_mark, dim3(nch), dim3(64), 0, c->stream, comp, (uint64_t)clen, Ent, Base, d_offsets,
                            (uint64_t)max_units, cst, fin);
         hipLaunchKernelGGL(k5d_result, dim3(1), dim3(64), 0, c->stream, nch, cst, c->k5res, d_offsets,

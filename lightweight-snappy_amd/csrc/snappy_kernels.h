@@ -70,10 +70,15 @@ __global__ void k4_decompress_back(const uint8_t *__restrict__ comp, const uint6
                                    int32_t *__restrict__ status);
 constexpr uint32_t K5_CHUNK = 16384;  // == K5_S in the kernels
 __global__ void k5a_chunk_walk(const uint8_t *__restrict__ comp, uint64_t clen, uint64_t *__restrict__ X,
-                               uint64_t *__restrict__ O);
+                               uint64_t *__restrict__ O, uint32_t *__restrict__ P);
+__global__ void k5b1_compose(const uint32_t *__restrict__ P, uint32_t nchunks, uint64_t *__restrict__ F);
 __global__ void k5b_carry(const uint8_t *__restrict__ comp, uint64_t clen, uint32_t nchunks,
-                          const uint64_t *__restrict__ X, const uint64_t *__restrict__ O, uint64_t *__restrict__ Ent,
+                          const uint64_t *__restrict__ X, const uint64_t *__restrict__ O, const uint64_t *__restrict__ F,
+                          uint64_t *__restrict__ BE, uint64_t *__restrict__ BB, uint64_t *__restrict__ Ent,
                           uint64_t *__restrict__ Base, int64_t *__restrict__ result);
+__global__ void k5b3_fill(const uint8_t *__restrict__ comp, uint64_t clen, const uint32_t *__restrict__ P,
+                          uint32_t nchunks, const uint64_t *__restrict__ BE, const uint64_t *__restrict__ BB,
+                          uint64_t *__restrict__ Ent, uint64_t *__restrict__ Base);
 __global__ void k5c_mark(const uint8_t *__restrict__ comp, uint64_t clen, const uint64_t *__restrict__ Ent,
                          const uint64_t *__restrict__ Base, uint64_t *__restrict__ offsets, uint64_t max_units,
                          int32_t *__restrict__ cst, uint64_t *__restrict__ fin);

@@ -2133,6 +2133,8 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l)
 // window starting before the chunk end reads at most 76 bytes past it), zero
 // at and past clen.  Byte r of the chunk (r relative to c0) is image byte r + o0.
 constexpr uint32_t K5_IMG = K5_S + 128;
+[[maybe_unused]] constexpr uint32_t kK5Esc = 0xFFFFFFFFu;  // K5a entry map: no fast successor
+[[maybe_unused]] constexpr uint64_t kK5Esc64 = ~0ull;      // K5b1 block map: no fast successor
 
 __device__ __forceinline__ void k5_stage(const uint8_t *__restrict__ comp, uint64_t clen, uint64_t c0, uint32_t *img,
                                          uint32_t lane)
@@ -2290,7 +2292,8 @@ __device__ __forceinline__ void k5_chain(const uint32_t *img, uint32_t o0, uint6
 
 #if SNAPPY_TU_DECODE
 __global__ __launch_bounds__(64) void k5a_chunk_walk(const uint8_t *__restrict__ comp, uint64_t clen,
-                                                     uint64_t *__restrict__ X, uint64_t *__restrict__ O)
+                                                     uint64_t *__restrict__ X, uint64_t *__restrict__ O,
+                                                     uint32_t *__restrict__ P)
 {
     // lane l: the chain entered at byte l of the chunk (every entry offset < 64
     // covered exactly; chains need not converge -- a periodic stream never
@@ -2340,6 +2343,12 @@ __global__ __launch_bounds__(64) void k5a_chunk_walk(const uint8_t *__restrict__
     }
     X[(uint64_t)c * 64 + lane] = c0 + x;
     O[(uint64_t)c * 64 + lane] = cum;
+    // the chunk's entry map for K5b1: the entry byte of the next chunk (< 64) |
+    // output << 8, or kK5Esc when either does not fit
+    const uint64_t nx = x - K5_S;
+    // (only into a full next chunk: an exit past clen, or a parse error, never composes)
+    P[(uint64_t)c * 64 + lane] = c0 + 2 * K5_S <= clen && x >= K5_S && nx < 64 && cum < (1u << 24)
+                                     ? (uint32_t)nx | ((uint32_t)cum << 8) : kK5Esc;
 }
 #endif
 
@@ -2349,10 +2358,45 @@ __global__ __launch_bounds__(64) void k5a_chunk_walk(const uint8_t *__restrict__
 [[maybe_unused]] constexpr uint32_t K5_G = SNAPPY_K5_G;  // chunks per prefetch group
 
 #if SNAPPY_TU_DECODE
+// K5b1: the entry maps of 64 consecutive chunks composed (block B = chunks
+// 64 B .. 64 B + 63): lane e follows the chain entered at byte e of the block's
+// first chunk through the block by one ds_bpermute per chunk (the row of chunk
+// c holds, per entry byte, the next chunk's entry byte | output << 8);
+// F[64 B + e] = exit entry byte into the next block | output << 8, or kK5Esc64.
+// A block with a short chunk (the stream's last) is never composed.
+__global__ __launch_bounds__(64) void k5b1_compose(const uint32_t *__restrict__ P, uint32_t nchunks,
+                                                   uint64_t *__restrict__ F)
+{
+    const uint32_t lane = threadIdx.x;
+    const uint32_t B = blockIdx.x;
+    uint32_t row[64];
+#pragma unroll
+    for (uint32_t j = 0; j < 64; j++)
+        row[j] = P[(uint64_t)__builtin_elementwise_min(64 * B + j, nchunks - 1) * 64 + lane];
+    uint32_t cur = lane;
+    uint64_t out = 0;
+    bool esc = 64 * B + 64 > nchunks;
+#pragma unroll
+    for (uint32_t j = 0; j < 64; j++) {
+        const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((cur & 63) << 2), (int)row[j]);
+        esc = esc || w == kK5Esc;
+        out += w >> 8;
+        cur = w & 0xFF;
+    }
+    F[64 * (uint64_t)B + lane] = esc ? kK5Esc64 : (uint64_t)cur | (out << 8);
+}
+
+// K5b2: one wave carries the true entry and output base through the stream:
+// a block whose entry byte is < 64, whose composed map has a fast successor
+// and that ends before N costs one readlane (its first chunk's entry and base
+// go to BE / BB for K5b3); any other block runs chunk by chunk (K5_G chunks per
+// prefetch group, entries < 64 by K5a's X / O, later ones walked, skipped
+// chunks marked) and writes its chunks' Ent / Base itself (BE = K5_SKIP).
 __global__ __launch_bounds__(64) void k5b_carry(const uint8_t *__restrict__ comp, uint64_t clen, uint32_t nchunks,
                                                 const uint64_t *__restrict__ X, const uint64_t *__restrict__ O,
-                                                uint64_t *__restrict__ Ent, uint64_t *__restrict__ Base,
-                                                int64_t *__restrict__ result)
+                                                const uint64_t *__restrict__ F, uint64_t *__restrict__ BE,
+                                                uint64_t *__restrict__ BB, uint64_t *__restrict__ Ent,
+                                                uint64_t *__restrict__ Base, int64_t *__restrict__ result)
 {
     const uint32_t lane = threadIdx.x;
     const K5Hdr h = k5_header(comp, clen);
@@ -2401,19 +2445,77 @@ __global__ __launch_bounds__(64) void k5b_carry(const uint8_t *__restrict__ comp
             }
         }
     };
-    const uint32_t ng = (nchunks + K5_G - 1) / K5_G;
-    load(0, xa, oa);
-    for (uint32_t g = 0; g < ng; g += 2) {
-        load(g + 1, xb, ob_);
-        run(g, xa, oa);
-        load(g + 2, xa, oa);
-        run(g + 1, xb, ob_);
+    static_assert(64 % K5_G == 0, "K5_G divides a 64-chunk block");
+    constexpr uint32_t kGB = 64 / K5_G;  // prefetch groups per block
+    const uint32_t nblk = (nchunks + 63) / 64;
+    uint64_t fr = F[lane];  // block 0's composed map, then each next one a block ahead
+    for (uint32_t B = 0; B < nblk; B++) {
+        const uint64_t fn = B + 1 < nblk ? F[64 * (uint64_t)(B + 1) + lane] : kK5Esc64;
+        const uint64_t c0 = h.len + (uint64_t)B * 64 * K5_S;
+        const uint64_t el = E - c0;
+        bool fast = false;
+        if (h.st == SNAPPY_ST_OK && base < N && el < 64) {
+            const uint64_t f = rl64(fr, (uint32_t)el);
+            if (f != kK5Esc64 && base + (f >> 8) < N) {
+                fast = true;
+                if (lane == 0) {
+                    BE[B] = E;
+                    BB[B] = base;
+                }
+                base += f >> 8;
+                E = c0 + 64 * (uint64_t)K5_S + (f & 0xFF);
+            }
+        }
+        if (!fast) {
+            if (lane == 0) BE[B] = K5_SKIP;
+            const uint32_t g0 = B * kGB;
+            load(g0, xa, oa);
+            for (uint32_t g = g0; g < g0 + kGB; g += 2) {
+                load(g + 1, xb, ob_);
+                run(g, xa, oa);
+                if (g + 2 < g0 + kGB) load(g + 2, xa, oa);
+                run(g + 1, xb, ob_);
+            }
+        }
+        fr = fn;
     }
     if (lane == 0) {
         result[0] = h.st;
         result[1] = (int64_t)N;
         result[2] = (int64_t)base;  // output the chain accounts for (== N for a whole stream)
     }
+}
+
+// K5b3: the chunks of every composed block get their entry and base by
+// following the block's entry through the 64 entry maps (one readlane each)
+__global__ __launch_bounds__(64) void k5b3_fill(const uint8_t *__restrict__ comp, uint64_t clen,
+                                                const uint32_t *__restrict__ P, uint32_t nchunks,
+                                                const uint64_t *__restrict__ BE, const uint64_t *__restrict__ BB,
+                                                uint64_t *__restrict__ Ent, uint64_t *__restrict__ Base)
+{
+    const uint32_t lane = threadIdx.x;
+    const uint32_t B = blockIdx.x;
+    const uint64_t e0 = BE[B];
+    if (e0 == K5_SKIP) return;  // K5b2 wrote this block chunk by chunk
+    const K5Hdr h = k5_header(comp, clen);
+    uint32_t row[64];
+#pragma unroll
+    for (uint32_t j = 0; j < 64; j++) row[j] = P[(uint64_t)(64 * B + j) * 64 + lane];  // composed: 64 full chunks
+    const uint64_t c0 = h.len + (uint64_t)B * 64 * K5_S;
+    uint32_t el = (uint32_t)(e0 - c0);
+    uint64_t base = BB[B], my_e = 0, my_b = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 64; j++) {
+        if (lane == j) {
+            my_e = c0 + (uint64_t)j * K5_S + el;
+            my_b = base;
+        }
+        const uint32_t w = __builtin_amdgcn_readlane(row[j], el);
+        base += w >> 8;
+        el = w & 0xFF;
+    }
+    Ent[64 * (uint64_t)B + lane] = my_e;
+    Base[64 * (uint64_t)B + lane] = my_b;
 }
 #endif
 

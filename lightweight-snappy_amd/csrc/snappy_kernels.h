@@ -68,7 +68,10 @@ __global__ void k4_decompress_back(const uint8_t *__restrict__ comp, const uint6
                                    uint64_t n, uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
                                    uint32_t ring, uint32_t bias, uint8_t *__restrict__ out,
                                    int32_t *__restrict__ status);
-constexpr uint32_t K5_CHUNK = 16384;  // == K5_S in the kernels
+#ifndef SNAPPY_K5_CHUNK
+#define SNAPPY_K5_CHUNK 16384
+#endif
+constexpr uint32_t K5_CHUNK = SNAPPY_K5_CHUNK;  // K5p chunk of compressed stream (K5_S in the kernels)
 __global__ void k5a_chunk_walk(const uint8_t *__restrict__ comp, uint64_t clen, uint64_t *__restrict__ X,
                                uint64_t *__restrict__ O, uint32_t *__restrict__ P);
 __global__ void k5b1_compose(const uint32_t *__restrict__ P, uint32_t nchunks, uint64_t *__restrict__ F);

@@ -2055,7 +2055,7 @@ __global__ __launch_bounds__(64) void k5_index_stream(const uint8_t *__restrict_
 //   K5d  first error in stream order, final offset.
 // Chunks entirely inside one element (long literals) are skipped.
 // ---------------------------------------------------------------------------
-[[maybe_unused]] constexpr uint32_t K5_S = 16384;
+[[maybe_unused]] constexpr uint32_t K5_S = SNAPPY_K5_CHUNK;
 [[maybe_unused]] constexpr uint64_t K5_SKIP = ~0ull;
 
 struct K5Hdr {

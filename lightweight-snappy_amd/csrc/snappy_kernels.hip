@@ -10,7 +10,7 @@
 //                          (:95-165; replaces the per-block fwrite :334-336)
 //   K4  k4_decompress_*    tag-dispatch decode, block-parallel
 //                          (src/snappy_decompression.c:290-363)
-//   K5  k5_* / k5a-d       block index of a foreign single stream
+//   K5  k5_* / k5a-d       block index of a foreign single stream (K5a, K5b1-3, K5c, K5d)
 //
 // The hash table holds block-relative positions; 0 is a valid candidate,
 // exactly as in the reference (snappy_compression.c:259-265).
@@ -2041,14 +2041,20 @@ __global__ __launch_bounds__(64) void k5_index_stream(const uint8_t *__restrict_
 // K5_S-byte chunks of compressed stream, each staged in LDS (chunk + halo):
 //   K5a  lane l walks the element chain entered at byte l of its chunk to the
 //        chunk end: its exit (first start at or past the end) and output.
-//        The 64 chains walk element by element to a checkpoint; chains through
-//        a common start coincide from there on, so when every unfinished lane
-//        stands on one start (text: always) the rest is ONE chain, walked by
-//        batch parse (every byte of a 64-byte window parsed as a candidate
-//        element, the chain found by pointer doubling over ds_bpermute, sizes
-//        and outputs by DPP scans); otherwise every lane walks on alone;
-//   K5b  one wave carries the true entry and output base through the chunks
-//        (an entry < 64 bytes in is a K5a lookup, a later one walks);
+//        The 64 chains walk element by element, checked at every 192-byte
+//        checkpoint; chains through a common start coincide from there on, so
+//        once every unfinished lane stands on one start (text: at once) the
+//        rest is ONE chain, walked by batch parse (every byte of a 64-byte
+//        window parsed as a candidate element, the chain found by pointer
+//        doubling over ds_bpermute, sizes and outputs by DPP scans).  K5a also
+//        writes the chunk's entry map (entry byte -> next chunk's entry byte |
+//        output << 8) for K5b1;
+//   K5b1 composes the maps of 64 consecutive chunks (one ds_bpermute per chunk);
+//   K5b2 (k5b_carry) one wave carries the true entry and output base over the
+//        blocks of 64 chunks (one readlane per composed block; chunk by chunk
+//        where a map escapes: an entry < 64 bytes in is a K5a lookup, a later
+//        one walks);
+//   K5b3 fills in the entry and base of every chunk of a composed block;
 //   K5c  every chunk re-walks its true chain from the true entry with the true
 //        output base by batch parse and records the element holding each
 //        multiple of 65,536 (with the checks of K5);

@@ -2142,25 +2142,39 @@ constexpr uint32_t K5_IMG = K5_S + 128;
 [[maybe_unused]] constexpr uint32_t kK5Esc = 0xFFFFFFFFu;  // K5a entry map: no fast successor
 [[maybe_unused]] constexpr uint64_t kK5Esc64 = ~0ull;      // K5b1 block map: no fast successor
 
-__device__ __forceinline__ void k5_stage(const uint8_t *__restrict__ comp, uint64_t clen, uint64_t c0, uint32_t *img,
-                                         uint32_t lane)
+// BYTES of stream from the 4-aligned absolute a0 into img (zero at and past clen)
+template <uint32_t BYTES>
+__device__ __forceinline__ void k5_stage_at(const uint8_t *__restrict__ comp, uint64_t clen, uint64_t a0, uint32_t *img,
+                                            uint32_t lane)
 {
-    const uint64_t a0 = c0 & ~3ull;
     uint32_t v[8];
-    for (uint32_t i0 = 0; i0 < K5_IMG / 4; i0 += 8 * 64) {
+    for (uint32_t i0 = 0; i0 < BYTES / 4; i0 += 8 * 64) {
 #pragma unroll
         for (uint32_t j = 0; j < 8; j++) {  // 8 loads per lane in flight
             const uint32_t i = i0 + 64 * j + lane;
-            v[j] = i < K5_IMG / 4 ? load_dw_guarded(comp, a0 + 4ull * i, clen) : 0u;
+            v[j] = i < BYTES / 4 ? load_dw_guarded(comp, a0 + 4ull * i, clen) : 0u;
         }
 #pragma unroll
         for (uint32_t j = 0; j < 8; j++) {
             const uint32_t i = i0 + 64 * j + lane;
-            if (i < K5_IMG / 4) img[i] = v[j];
+            if (i < BYTES / 4) img[i] = v[j];
         }
     }
     __syncthreads();
 }
+
+__device__ __forceinline__ void k5_stage(const uint8_t *__restrict__ comp, uint64_t clen, uint64_t c0, uint32_t *img,
+                                         uint32_t lane)
+{
+    k5_stage_at<K5_IMG>(comp, clen, c0 & ~3ull, img, lane);
+}
+
+// K5c's image: a WIN-byte window (+ 128) re-staged as its chain moves on, so
+// K5c holds 4.2 KiB of LDS (32 waves per CU) instead of the whole chunk
+#ifndef SNAPPY_K5_WIN
+#define SNAPPY_K5_WIN 4096
+#endif
+constexpr uint32_t K5_WIN = SNAPPY_K5_WIN;
 
 // the element at image byte q (rem = stream bytes from it to clen): as k5_parse
 __device__ __forceinline__ bool k5_parse_img(const uint32_t *img, uint32_t q, uint64_t rem, uint64_t &size,
@@ -2193,15 +2207,23 @@ __device__ __forceinline__ bool k5_parse_img(const uint32_t *img, uint32_t q, ui
 // walk (an element holding a multiple of 65,536 strictly inside it gets a
 // straddle entry, one ending on it the entry of its successor); any error
 // leaves st set (the index is then discarded, so extra entries are harmless).
-template <bool MARK>
-__device__ __forceinline__ void k5_chain(const uint32_t *img, uint32_t o0, uint64_t c0, uint64_t clen, uint32_t end_rel,
-                                         uint64_t &x, uint64_t &op, uint64_t N, uint64_t *__restrict__ offsets,
-                                         uint64_t max_units, int32_t &st, uint32_t lane)
+// The image holds the stream from the absolute 4-aligned ia on; WIN > 0: it
+// is a WIN + 128-byte window, re-staged at the chain when the chain leaves it.
+template <bool MARK, uint32_t WIN>
+__device__ __forceinline__ void k5_chain(const uint8_t *__restrict__ comp, uint32_t *img, uint64_t &ia, uint64_t c0,
+                                         uint64_t clen, uint32_t end_rel, uint64_t &x, uint64_t &op, uint64_t N,
+                                         uint64_t *__restrict__ offsets, uint64_t max_units, int32_t &st, uint32_t lane)
 {
     while (x < end_rel && (!MARK || op < N) && st == SNAPPY_ST_OK) {
+        if constexpr (WIN > 0) {
+            if (c0 + x >= ia + WIN) {  // a window's reads end before ia + WIN + 72
+                ia = (c0 + x) & ~3ull;
+                k5_stage_at<WIN + 128>(comp, clen, ia, img, lane);
+            }
+        }
         const uint32_t r = (uint32_t)x + lane;
         uint64_t size, len;
-        const bool ok = k5_parse_img(img, r + o0, c0 + r < clen ? clen - (c0 + r) : 0, size, len);
+        const bool ok = k5_parse_img(img, (uint32_t)(c0 + r - ia), c0 + r < clen ? clen - (c0 + r) : 0, size, len);
         // element chain from lane 0 by pointer doubling: lane k <- start of element k
         const uint32_t nx = lane + (size < 64 ? (uint32_t)size : 64u);
 #define K5JUMP(T, idx) ({ const uint32_t _i = (idx);                                                  \
@@ -2339,7 +2361,8 @@ __global__ __launch_bounds__(64) void k5a_chunk_walk(const uint8_t *__restrict__
         if (!__ballot(x < end_rel && (uint32_t)x != x1)) {
             uint64_t xe = x1, oe = 0;
             int32_t st = SNAPPY_ST_OK;
-            k5_chain<false>(img, o0, c0, clen, end_rel, xe, oe, 0, nullptr, 0, st, lane);
+            uint64_t ia = c0 & ~3ull;
+            k5_chain<false, 0>(comp, img, ia, c0, clen, end_rel, xe, oe, 0, nullptr, 0, st, lane);
             if (x < end_rel) {
                 x = xe;
                 cum += oe;
@@ -2531,7 +2554,7 @@ __global__ __launch_bounds__(64) void k5c_mark(const uint8_t *__restrict__ comp,
                                                uint64_t *__restrict__ offsets, uint64_t max_units,
                                                int32_t *__restrict__ cst, uint64_t *__restrict__ fin)
 {
-    __shared__ uint32_t img[K5_IMG / 4 + 4];
+    __shared__ uint32_t img[(K5_WIN ? K5_WIN + 128 : K5_IMG) / 4 + 4];
     const uint32_t lane = threadIdx.x;
     const uint32_t c = blockIdx.x;
     const K5Hdr h = k5_header(comp, clen);
@@ -2542,9 +2565,15 @@ __global__ __launch_bounds__(64) void k5c_mark(const uint8_t *__restrict__ comp,
         const uint64_t units = (N + SNAPPY_BLOCK - 1) / SNAPPY_BLOCK;
         const uint64_t c0 = h.len + (uint64_t)c * K5_S;
         const uint32_t end_rel = (uint32_t)(c0 + K5_S < clen ? K5_S : clen - c0);
-        k5_stage(comp, clen, c0, img, lane);
-        uint64_t op = Base[c], xr = x - c0;
-        k5_chain<true>(img, (uint32_t)(c0 & 3), c0, clen, end_rel, xr, op, N, offsets, max_units, st, lane);
+        uint64_t op = Base[c], xr = x - c0, ia;
+        if constexpr (K5_WIN > 0) {
+            ia = x & ~3ull;  // from the true entry on
+            k5_stage_at<K5_WIN + 128>(comp, clen, ia, img, lane);
+        } else {
+            ia = c0 & ~3ull;
+            k5_stage(comp, clen, c0, img, lane);
+        }
+        k5_chain<true, K5_WIN>(comp, img, ia, c0, clen, end_rel, xr, op, N, offsets, max_units, st, lane);
         x = c0 + xr;
         if (st == SNAPPY_ST_OK && op == N && lane == 0) {
             if (units < max_units) offsets[units] = x;

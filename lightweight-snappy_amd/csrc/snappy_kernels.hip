@@ -2352,7 +2352,10 @@ __global__ __launch_bounds__(64) void k5a_chunk_walk(const uint8_t *__restrict__
     };
     // checkpoints every kCheck bytes: as soon as the unfinished lanes stand on
     // one start, the rest is one batch-parsed chain
-    constexpr uint32_t kCheck = 192;
+#ifndef SNAPPY_K5_CHECK
+#define SNAPPY_K5_CHECK 192
+#endif
+    constexpr uint32_t kCheck = SNAPPY_K5_CHECK;
     for (uint32_t lim = kCheck;; lim += kCheck) {
         walk_to(end_rel < lim ? end_rel : lim);
         const uint64_t open = __ballot(x < end_rel);

@@ -59,13 +59,14 @@ int main(int argc, char *argv[])
         else if (opt == 'i') indexed = 1;
         else usage();
     }
+    if (indexed && mode == M_BST) usage();  /* -b writes no block index */
     const char *in_name = argv[argc - 2], *out_name = argv[argc - 1];
     FILE *in = open_or_die(in_name, "rb");
     FILE *out = open_or_die(out_name, "wb");
     unsigned long long in_size = file_size(in);
     FILE *idx = NULL;
-    if (indexed && mode != M_BST) {
-        char name[4096];
+    char name[4096] = "";
+    if (indexed) {
         snprintf(name, sizeof(name), "%s.idx", mode == M_COMPRESS ? out_name : in_name);
         idx = open_or_die(name, mode == M_COMPRESS ? "wb" : "rb");
     }
@@ -89,6 +90,7 @@ int main(int argc, char *argv[])
     fclose(in);
     fclose(out);
     if (idx) fclose(idx);
+    if (rc != 0 && idx && mode == M_COMPRESS) remove(name);  /* no partial index left behind */
     double secs = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
     if (show) {
         FILE *o = open_or_die(out_name, "rb");

@@ -35,11 +35,13 @@ struct snappy_amd_ctx {
     int32_t *h_status = nullptr;    // pinned, grows with status_cap
     size_t h_status_cap = 0;
     size_t last_units = 0;
+    int last_layout = SNAPPY_AMD_SINGLE;  // of the last decode launch (status mapping)
     // host-buffer path staging
     uint8_t *d_a = nullptr; size_t d_a_cap = 0;
     uint8_t *d_b = nullptr; size_t d_b_cap = 0;
     uint64_t *d_idx = nullptr; size_t d_idx_cap = 0;
     uint8_t *k5buf = nullptr; size_t k5buf_cap = 0;  // chunk-parallel index scratch
+    uint8_t *k5copy = nullptr; size_t k5copy_cap = 0;  // aligned copy of a misaligned stream
     bool timing = false;
     hipEvent_t ev[5] = {};
     float k1_ms = 0, k3_ms = 0, k4_ms = 0;
@@ -113,7 +115,7 @@ void snappy_amd_destroy(snappy_amd_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void *bufs[] = {c->sizes, c->tokens, c->ntok, c->seg_off, c->status, c->total, c->k5res,
-                    c->d_a, c->d_b, c->d_idx, c->k5buf};
+                    c->d_a, c->d_b, c->d_idx, c->k5buf, c->k5copy};
     for (void *b : bufs) if (b) (void)hipFree(b);
     if (c->h_total) (void)hipHostFree(c->h_total);
     if (c->h_status) (void)hipHostFree(c->h_status);
@@ -293,6 +295,7 @@ static int decompress_launch(snappy_amd_ctx *c, const void *d_comp, const uint64
     }
     if (c->timing) (void)hipEventRecord(c->ev[4], c->stream);
     c->last_units = units;
+    c->last_layout = layout;
     return SNAPPY_AMD_OK;
 }
 
@@ -313,9 +316,11 @@ int snappy_amd_decompress_status(snappy_amd_ctx *c)
     HIP_OK(hipStreamSynchronize(c->stream));
     if (c->timing) (void)hipEventElapsedTime(&c->k4_ms, c->ev[3], c->ev[4]);
     for (size_t i = 0; i < c->last_units; i++) {
-        // DEFER survives only in a STREAMS unit (no pass 2): a copy reaching
-        // before the start of its own stream
-        if (c->h_status[i] > 0) return SNAPPY_AMD_ERR_OFFSET;
+        // DEFER survives a STREAMS launch (no pass 2) only for a copy reaching
+        // before the start of its own stream; after a SINGLE launch pass 2 ends
+        // every deferred unit, so a DEFER left over is an internal failure
+        if (c->h_status[i] > 0) return c->last_layout == SNAPPY_AMD_STREAMS ? SNAPPY_AMD_ERR_OFFSET
+                                                                            : SNAPPY_AMD_ERR_DEVICE;
         if (c->h_status[i] != SNAPPY_ST_OK) return c->h_status[i];
     }
     return SNAPPY_AMD_OK;
@@ -351,7 +356,17 @@ int snappy_amd_index_device(snappy_amd_ctx *c, const void *d_comp, size_t clen, 
     HIP_OK(hipSetDevice(c->device));
     const uint8_t *comp = static_cast<const uint8_t *>(d_comp);
     const bool serial = getenv("SNAPPY_AMD_K5_SERIAL") != nullptr;  // read per call (tests toggle it)
-    if (serial || clen < 4 * (size_t)K5_CHUNK || (reinterpret_cast<uintptr_t>(d_comp) & 3)) {
+    if (!serial && clen >= 4 * (size_t)K5_CHUNK && (reinterpret_cast<uintptr_t>(d_comp) & 3)) {
+        // K5p stages 4-aligned dwords of the stream: a stream at an odd address
+        // is first moved to an aligned scratch copy (one HBM pass, a few % of
+        // the index time) instead of falling back to the one-wave serial walk;
+        // the index entries are stream-relative, so they are the same
+        int rc = grow(reinterpret_cast<void **>(&c->k5copy), &c->k5copy_cap, clen + 16);
+        if (rc) return rc;
+        HIP_OK(hipMemcpyAsync(c->k5copy, d_comp, clen, hipMemcpyDeviceToDevice, c->stream));
+        comp = c->k5copy;
+    }
+    if (serial || clen < 4 * (size_t)K5_CHUNK) {
         hipLaunchKernelGGL(k5_index_stream, dim3(1), dim3(64), 0, c->stream, comp, (uint64_t)clen, d_offsets,
                            (uint64_t)max_units, c->k5res);
     } else {
@@ -564,6 +579,9 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
     if ((rc = slot_drain(g_slots[last ^ 1], fout, fidx, &base))) return rc;
     if ((rc = slot_drain(g_slots[last], fout, fidx, &base))) return rc;
     if (fidx) {
+        // the stream's preamble says header_value; an index is only valid for a
+        // stream whose preamble is the length actually compressed
+        if (total_in != header_value) return SNAPPY_AMD_ERR_INDEX;
         const uint64_t units = (total_in + SNAPPY_AMD_BLOCK - 1) / SNAPPY_AMD_BLOCK;
         const uint64_t cnt = total_in ? units + 1 : 0;
         if (total_in && fwrite(&base, sizeof(uint64_t), 1, fidx) != 1) return SNAPPY_AMD_ERR_IO;
@@ -602,8 +620,12 @@ int snappy_amd_host_decompress_idx(const uint8_t *in, size_t n, const uint64_t *
     if ((rc = grow(reinterpret_cast<void **>(&c->d_idx), &c->d_idx_cap, (units + 2) * sizeof(uint64_t)))) return rc;
     HIP_OK(hipMemcpyAsync(c->d_a, in, n, hipMemcpyHostToDevice, c->stream));
     if (idx) {  // a sidecar index: no index pass; it must describe this stream
-        if (count != units + 1 || (idx[units] & ((1ull << SNAPPY_AMD_IDX_OFFSET_BITS) - 1)) != n)
-            return SNAPPY_AMD_ERR_INDEX;
+        // every entry, not just the last: offsets inside the stream, never
+        // decreasing, ending at its length (a tampered .idx is refused here)
+        const uint64_t off_mask = (1ull << SNAPPY_AMD_IDX_OFFSET_BITS) - 1;
+        if (count != units + 1 || (idx[units] & off_mask) != n) return SNAPPY_AMD_ERR_INDEX;
+        for (size_t i = 0; i < units; i++)
+            if ((idx[i] & off_mask) > (idx[i + 1] & off_mask)) return SNAPPY_AMD_ERR_INDEX;
         HIP_OK(hipMemcpyAsync(c->d_idx, idx, count * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
     } else {
         size_t got = 0;

@@ -112,7 +112,9 @@ static int read_index(FILE *f, uint64_t **entries, size_t *count)
     if (h[2] > (h[1] >> 16) + 2) return SNAPPY_AMD_ERR_INDEX;
     uint64_t *e = (uint64_t *)malloc((h[2] ? h[2] : 1) * sizeof(uint64_t));
     if (!e) return SNAPPY_AMD_ERR_IO;
-    if (fread(e, sizeof(uint64_t), h[2], f) != h[2]) { free(e); return SNAPPY_AMD_ERR_INDEX; }
+    /* exactly count entries: a short file or trailing bytes are refused (as by
+     * snappy_amd.read_index) */
+    if (fread(e, sizeof(uint64_t), h[2], f) != h[2] || fgetc(f) != EOF) { free(e); return SNAPPY_AMD_ERR_INDEX; }
     *entries = e;
     *count = (size_t)h[2];
     return SNAPPY_AMD_OK;

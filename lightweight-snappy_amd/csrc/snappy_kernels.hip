@@ -847,6 +847,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #undef LDS_ORDER
 #undef CAND_LANES
 #undef K1R_COUNT
+    // BIG: the last stage() may still be writing ring_stage; drain it before the
+    // workgroup's LDS can be released (tools/check_asm_waits.py checks every path)
+    if constexpr (BIG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     flush_tokens();
     // the tail literal is pseudo-token nt (src/snappy_compression.c:292-297)
     if (lane == 0) {
@@ -1454,8 +1457,11 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     int32_t st = SNAPPY_ST_OK;
     // the unit's compressed bytes: up to the next entry, or (its last element
     // straddling out) as far as the stream goes
-    uint64_t c1 = c1n;
-    if (skip1) c1 = (offsets[(n + unit - 1) / unit] & kIdxOffMask) + bias;
+    // (the last entry is the stream end: no read goes past it, whatever the
+    // entries in between say -- a corrupt index fails as TRUNCATED, not a fault)
+    const uint64_t c_end = (offsets[(n + unit - 1) / unit] & kIdxOffMask) + bias;
+    uint64_t c1 = skip1 ? c_end : c1n;
+    if (c1 > c_end) c1 = c_end;
     if (c1 > c0 + 0x7FFFFFFFull) c1 = c0 + 0x7FFFFFFFull;
     if (c1 < c0 || ((skip0 | skip1) && !allow_back)) st = SNAPPY_ST_TRUNCATED;
     const uint32_t clen = st == SNAPPY_ST_OK ? (uint32_t)(c1 - c0) : 0u;

@@ -204,7 +204,10 @@ def decompress(data) -> bytes:
 def read_index(data: bytes):
     """Sidecar index file (snappy_amd.h) -> (N, [entries])."""
     import struct
+    if len(data) < 24:
+        raise SnappyError(ERR_INDEX, "read_index")
     magic, n, count = struct.unpack_from("<QQQ", data, 0)
+    # exactly `count` entries, no trailing bytes (the C reader refuses them too)
     if magic != IDX_MAGIC or len(data) != 24 + 8 * count:
         raise SnappyError(ERR_INDEX, "read_index")
     return n, list(struct.unpack_from(f"<{count}Q", data, 24))

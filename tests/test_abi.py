@@ -139,3 +139,46 @@ def test_kernel_register_budget(tmp_path):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import check_ring
     assert check_ring.check(dis) == []
+
+
+@pytest.mark.parametrize("obj", ["snappy_kernels_c.o", "snappy_kernels_d.o"])
+def test_asm_memory_ops_drained(tmp_path, obj):
+    """Inline-asm memory operations (the round-2 hang class):
+    every asm load into a register waits inside its own asm block, and every
+    LDS-DMA (global_load_lds) is drained by s_waitcnt vmcnt(0) on every path
+    to s_endpgm of the built code object (tools/check_asm_waits.py)."""
+    import shutil
+    import sys
+    llvm = "/opt/rocm/lib/llvm/bin"
+    path = os.path.join(ROOT, "lightweight-snappy_amd", "build", obj)
+    if not (os.path.exists(path) and os.path.exists(f"{llvm}/llvm-objdump") and shutil.which("objcopy")):
+        pytest.skip("needs the in-tree build object and the ROCm LLVM tools")
+    fat, co = tmp_path / "fat.bin", tmp_path / "k.co"
+    subprocess.run(["objcopy", f"--dump-section=.hip_fatbin={fat}", path], check=True)
+    subprocess.run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+    dis = subprocess.run([f"{llvm}/llvm-objdump", "-d", str(co)], check=True, capture_output=True, text=True).stdout
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import check_asm_waits
+    assert "global_load_lds" in dis or obj.endswith("_d.o")  # the checker sees the compress kernels' DMA
+    assert check_asm_waits.check(dis) == []
+    csrc = os.path.join(ROOT, "lightweight-snappy_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith(".hip"):
+            assert check_asm_waits.lint_source(os.path.join(csrc, f)) == [], f
+
+
+def test_asm_wait_checker_catches_undrained_dma():
+    """The checker itself: a synthetic kernel whose LDS-DMA can reach s_endpgm
+    through a branch that skips the wait is flagged; the drained one is not."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import check_asm_waits
+    k = ("0000000000001000 <kern>:\n"
+         "\tglobal_load_lds_dword v1, s[2:3]      // 000000001000: 0\n"
+         "\ts_cbranch_scc1 2                      // 000000001008: 0 <kern+0x14>\n"
+         "\ts_waitcnt vmcnt(0)                    // 00000000100C: 0\n"
+         "\ts_nop 0                               // 000000001010: 0\n"
+         "\ts_endpgm                              // 000000001014: 0\n")
+    assert len(check_asm_waits.check(k)) == 1
+    assert check_asm_waits.check(k.replace("s_cbranch_scc1 2", "s_nop 1")) == []

@@ -3,20 +3,34 @@
 
 One step = one compress (K1r match finder + K3 scan + K2 emit) and one
 decompress (K4) of the rank's batch, inputs already resident in HBM.
-Default workload = BASELINE.json configs[1]: 1 GiB of synthetic enwik8-like
-text as 32,768 independent 32 KiB streams (each == the reference's
-snappy_compress() of its chunk), per GPU (weak scaling: every rank gets its
-own 1 GiB shard of the generator).  --total-bytes T instead fixes the job
-size (strong scaling, configs[3]: 64 GiB over 1/2/4/8 GPUs): rank r owns
-the unit-aligned range dist.shard_range(T, N, r) of the generator.
+
+Workloads (BASELINE.json configs):
+  N = 1, default   configs[1]: 1 GiB of synthetic enwik8-like text as 32,768
+                   independent 32 KiB streams (each == the reference's
+                   snappy_compress() of its chunk).  The same JSON line then
+                   carries compact sub-results for the other single-GPU
+                   configs -- text64k (one snappy_compress() stream of 64 KiB
+                   blocks), random + repeat (configs[2]), decode10g
+                   (configs[4]) -- and host_file_api, the FILE* entry points
+                   cmd.c calls, on a 4 GiB file in /dev/shm.
+  N > 1, default   configs[3]: 64 GiB of 32 KiB text streams in total,
+                   strong-scaled over the N ranks (rank r owns the
+                   unit-aligned range dist.shard_range(64 GiB, N, r)).
+  --weak           N > 1 with --bytes-per-gpu per rank instead.
+  --total-bytes T  any fixed job size (the N = 1 point of configs[3] is
+                   --gpus 1 --total-bytes 68719476736).
 
 Exchange steps: C1, the all-gather of the shard sizes, is part
-of every step; with N > 1 the run then times, outside the steps, C2 (the
-RCCL all-gather that reassembles the compressed stream on every rank) and
-C3 (the all-gather of the decoded shards), each verified by checksums.
+of every step.  With N > 1 a second timed loop runs the whole job end to
+end -- compress, C1, C2 (RCCL all-gather of the compressed shards, padded:
+RCCL has no all-gatherv), compaction into the contiguous stream every rank
+then holds, decompress of the rank's blocks from that stream -- and reports
+it as `value_end_to_end`.  C3 (all-gather of the decoded shards) is opt-in
+(--c3).  Every phase is checked (round trip, per-shard checksums).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-                       [--workload text32k|text64k|random|repeat|decode10g] [--total-bytes T]
+                       [--workload text32k|text64k|random|repeat|decode10g]
+                       [--total-bytes T | --weak [--bytes-per-gpu B]]
 --gpus N without a torch.distributed launcher spawns the N ranks itself
 (python -m torch.distributed.run, 127.0.0.1); this parent process never
 touches the GPU.
@@ -24,11 +38,13 @@ touches the GPU.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import socket
 import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -41,10 +57,12 @@ import torch.distributed as dist  # noqa: E402
 
 import datagen  # noqa: E402
 import snappy_amd  # noqa: E402
-from dist import shard_range  # noqa: E402
+from dist import HBM_BYTES, pieces_of, rank_plan, shard_range  # noqa: E402
 
 METRIC = "compress + decompress MB/s at 1/2/4/8 MI355X; % HBM roofline; ratio vs ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+GiB = 1 << 30
+CONFIG3_BYTES = 64 * GiB  # BASELINE configs[3]: 64 GB of 32 KB blocks over 1/2/4/8 GPUs
 
 WORKLOADS = {
     # name: (generator kind, seed, layout, chunk, description)
@@ -60,10 +78,10 @@ WORKLOADS = {
 }
 DECODE_ONLY = {"decode10g"}
 DECODE10G_BYTES = (18_500_000_000 // 65536) * 65536  # ratio ~1.85 -> ~10 GB of compressed stream
-GiB = 1 << 30
+SUB_WORKLOADS = ("text64k", "random", "repeat", "decode10g")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -71,31 +89,47 @@ def parse():
     ap.add_argument("--workload", default="text32k", choices=sorted(WORKLOADS))
     ap.add_argument("--bytes-per-gpu", type=int, default=GiB, help="weak scaling: input bytes per rank")
     ap.add_argument("--total-bytes", type=int, default=0,
-                    help="strong scaling: fixed job size sharded over the ranks (e.g. 68719476736 = configs[3])")
-    ap.add_argument("--piece-bytes", type=int, default=16 * GiB,
+                    help="strong scaling: fixed job size sharded over the ranks (default with N > 1: "
+                         "68719476736 = configs[3])")
+    ap.add_argument("--weak", action="store_true", help="N > 1: --bytes-per-gpu per rank instead of configs[3]")
+    ap.add_argument("--piece-bytes", type=int, default=8 * GiB,
                     help="a rank compresses its range in pieces of at most this many bytes (bounds token scratch)")
-    ap.add_argument("--no-assemble", action="store_true", help="N > 1: skip the timed C2/C3 all-gathers")
+    ap.add_argument("--no-assemble", action="store_true", help="N > 1: skip the end-to-end loop with C2")
+    ap.add_argument("--c3", action="store_true", help="N > 1: also time C3, the all-gather of the decoded shards")
+    ap.add_argument("--e2e-steps", type=int, default=3, help="N > 1: steps of the end-to-end loop")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-host-e2e", action="store_true", help="skip the PCIe-inclusive host API sample")
+    ap.add_argument("--no-host-e2e", action="store_true", help="skip the PCIe-inclusive host API samples")
+    ap.add_argument("--no-sub", action="store_true", help="N = 1: skip the sub-results of the other configs")
+    ap.add_argument("--file-api-bytes", type=int, default=4 * GiB, help="host_file_api: size of the /dev/shm file")
     ap.add_argument("--keep-size", action="store_true", help="decode10g: use --bytes-per-gpu as given")
+    ap.add_argument("--dist-world1", action="store_true",
+                    help="N = 1: still create the process group and run the end-to-end exchange loop (1 rank)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL, the real path) or gloo (CPU collectives; rehearsal with ranks sharing a GPU)")
     ap.add_argument("--cpu-sample-bytes", type=int, default=GiB)
     ap.add_argument("--pmc", default=None,
                     help="rocprofv3 PMC summary giving HBM traffic per launch (default profiles/pmc_<workload>.json, "
                          "written by tools/pmc_summary.py)")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
     if a.pmc is None:
-        a.pmc = os.path.join(ROOT, "profiles", f"pmc_{a.workload}.json")
+        a.pmc = pmc_path(a.workload)
     return a
+
+
+def pmc_path(workload: str) -> str:
+    return os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def spawn_ranks(n: int) -> int:
     """--gpus N outside a launcher: run N ranks under torch.distributed.run
     (a child process; nothing here has touched the GPU)."""
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    port = _free_port()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
@@ -127,7 +161,8 @@ def cpu_model() -> str:
     return ""
 
 
-def cpu_baseline(kind: str, seed: int, chunk: int, layout: int, sample: int, decode_only: bool = False):
+def cpu_baseline(kind: str, seed: int, chunk: int, layout: int, sample: int, decode_only: bool = False,
+                 all_cores: bool = True):
     """The oracle (CPU restatement, fixture-verified bit-exact with the
     reference) timed on this host, 1 thread like the reference, wall clock;
     then over every core of this process's CPU share."""
@@ -152,6 +187,8 @@ def cpu_baseline(kind: str, seed: int, chunk: int, layout: int, sample: int, dec
             "sample": f"{a.size / 2**20:.0f} MiB of the same workload, compress {a.size / (t1 - t0) / 1e6:.1f} MB/s"
                       f" + decompress {a.size / (t2 - t1) / 1e6:.1f} MB/s, oracle/snappy_oracle.c -O2, 1 thread,"
                       f" {cpu_model()}"}
+    if not all_cores:
+        return base, None
     # every host core this process may use, over independent units
     threads, note = cpu_share()
     t0 = time.perf_counter()
@@ -201,7 +238,6 @@ def host_end_to_end(kind: str, seed: int, sample: int) -> dict:
     """PCIe-inclusive rate of the drop-in host API (snappy_compress_buffer /
     snappy_decompress_buffer: one SINGLE stream of 64 KiB blocks, pageable
     host buffers in and out).  Reported beside `value`, never as it."""
-    import ctypes
     lib = snappy_amd.lib()
     a = datagen.make(kind, sample, seed)
     cap = snappy_amd.max_compressed_length(a.size)
@@ -224,6 +260,55 @@ def host_end_to_end(kind: str, seed: int, sample: int) -> dict:
     assert np.array_equal(back, a)
     return {"bytes": int(a.size), "layout": "SINGLE 64 KiB blocks", "compress_MBps": round(a.size / best_c / 1e6, 1),
             "decompress_MBps": round(a.size / best_d / 1e6, 1), "note": "pageable host buffers, H2D+D2H included"}
+
+
+def host_file_api(nbytes: int) -> dict:
+    """The path src/cmd.c:90-98 actually calls: snappy_compress(FILE*, size,
+    FILE*) and snappy_decompress(FILE*, FILE*) of libsnappy_amd.so, on an
+    nbytes text file in /dev/shm (page cache, so the disk is not what is
+    measured), in-process through libc stdio (no process start in the time).
+    MB/s = uncompressed bytes / wall second, as src/result.c prints them.
+    The output is checked byte for byte against the input."""
+    lib = snappy_amd.lib()
+    libc = ctypes.CDLL(None)
+    libc.fopen.restype = ctypes.c_void_p
+    libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    libc.fclose.argtypes = [ctypes.c_void_p]
+    d = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    with tempfile.TemporaryDirectory(dir=d, prefix="snappy_bench_") as tmp:
+        src, snp, dec = (os.path.join(tmp, x).encode() for x in ("in", "in.snp", "in.dec"))
+        a = np.empty(nbytes, dtype=np.uint8)
+        datagen.fill(a, "T", 1234, threads=16)
+        a.tofile(src.decode())
+        del a
+
+        def run(fn, *files, size=None):
+            fi = libc.fopen(files[0], b"rb")
+            fo = libc.fopen(files[1], b"wb")
+            assert fi and fo
+            t0 = time.perf_counter()
+            rc = fn(ctypes.c_void_p(fi), ctypes.c_ulonglong(size), ctypes.c_void_p(fo)) if size is not None else \
+                fn(ctypes.c_void_p(fi), ctypes.c_void_p(fo))
+            libc.fclose(ctypes.c_void_p(fo))
+            t = time.perf_counter() - t0
+            libc.fclose(ctypes.c_void_p(fi))
+            return rc, t
+
+        best_c = best_d = float("inf")
+        for _ in range(2):  # the first round also allocates the pipeline's pinned slots
+            _, tc = run(lib.snappy_compress, src, snp, size=nbytes)
+            assert lib.snappy_amd_last_status() == 0
+            rc, td = run(lib.snappy_decompress, snp, dec)
+            assert rc == 0 and lib.snappy_amd_last_status() == 0, rc
+            best_c, best_d = min(best_c, tc), min(best_d, td)
+        clen = os.path.getsize(snp.decode())
+        ok = os.path.getsize(dec.decode()) == nbytes and \
+            np.array_equal(np.fromfile(dec.decode(), dtype=np.uint8), np.fromfile(src.decode(), dtype=np.uint8))
+    return {"bytes": nbytes, "file": "/dev/shm" if d else "tmp", "compressed_bytes": clen,
+            "compress_MBps": round(nbytes / best_c / 1e6, 1), "decompress_MBps": round(nbytes / best_d / 1e6, 1),
+            "round_trip_ok": bool(ok),
+            "note": "snappy_compress / snappy_decompress FILE* entry points (cmd.c's calls), text, best of 2, "
+                    "file I/O + PCIe + kernels"}
 
 
 def hbm_copy_gbps(dev, nbytes: int = GiB) -> float:
@@ -250,12 +335,28 @@ def checksum(t: torch.Tensor) -> int:
     k = 8192
     w = torch.arange(1, k + 1, device=t.device, dtype=torch.int64)
     m = n - n % k
-    body = t[:m].view(-1, k).to(torch.int64)
-    rows = (body * w).sum(dim=1)
-    s = int((rows * torch.arange(1, rows.numel() + 1, device=t.device, dtype=torch.int64)).sum()) if m else 0
+    s = 0
+    # in 16 MiB slices, so the int64 temporaries stay small next to a 32 GiB shard
+    for o in range(0, m, 1 << 24):
+        e = min(m, o + (1 << 24))
+        body = t[o:e].view(-1, k).to(torch.int64)
+        rows = (body * w).sum(dim=1)
+        r0 = o // k
+        s += int((rows * torch.arange(r0 + 1, r0 + rows.numel() + 1, device=t.device, dtype=torch.int64)).sum())
     tail = t[m:].to(torch.int64)
     s += int((tail * w[: tail.numel()]).sum()) * 7919 + n
     return s & ((1 << 62) - 1)
+
+
+def load_pmc(path: str, workload: str, n: int) -> dict:
+    """{kernel: hbm_bytes per launch} of a tools/pmc_summary.py file for this workload and size."""
+    try:
+        pm = json.load(open(path))
+        if pm.get("workload") == workload and pm.get("bytes_per_gpu") == n:
+            return {k: v.get("hbm_bytes") for k, v in pm["kernels"].items()}
+    except (OSError, ValueError, KeyError):
+        pass
+    return {}
 
 
 class Piece:
@@ -270,6 +371,215 @@ class Piece:
         self.offs = None
 
 
+class Job:
+    """One workload's buffers on this rank: the input range in HBM, the payload
+    (sized for the job's largest shard, equal on every rank), the decoded
+    output and the per-piece block indexes."""
+
+    def __init__(self, name, codec, dev, n, r_off, total_in, n_max, piece_bytes, keep_size=False):
+        kind, seed, layout, chunk, desc = WORKLOADS[name]
+        self.name, self.kind, self.seed, self.layout, self.chunk, self.desc = name, kind, seed, layout, chunk, desc
+        self.codec, self.dev = codec, dev
+        self.decode_only = name in DECODE_ONLY
+        self.unit = chunk if layout == snappy_amd.STREAMS else 65536
+        self.n, self.r_off, self.total_in = n, r_off, total_in
+        # the rank's range in HBM, generated on the host 1 GiB at a time
+        self.x = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+        host = np.empty(min(max(n, 1), GiB), dtype=np.uint8)
+        for o in range(0, n, GiB):
+            m = min(GiB, n - o)
+            datagen.fill(host[:m], kind, seed, offset=r_off + o, threads=16)
+            self.x[o:o + m].copy_(torch.from_numpy(host[:m]))
+        del host
+        self.units = codec.num_units(n, chunk, layout)
+        self.pieces = []
+        o = 0
+        for m in pieces_of(n, self.unit, piece_bytes):
+            flags = snappy_amd.NO_PREAMBLE if (layout == snappy_amd.SINGLE and (r_off + o) > 0) else 0
+            self.pieces.append(Piece(o, m, flags))
+            o += m
+        cap = sum(codec.max_output(m, chunk, layout) for m in pieces_of(n_max, self.unit, piece_bytes))
+        self.out_cap = max(cap, 16)
+        self.out = torch.empty(self.out_cap, dtype=torch.uint8, device=dev)
+        for p in self.pieces:
+            p.offs = torch.empty(codec.num_units(p.n, chunk, layout) + 1, dtype=torch.int64, device=dev)
+        self.back = torch.empty(max(n_max, 1), dtype=torch.uint8, device=dev)
+        # SINGLE layout: the stream's first piece carries the global preamble
+        self.header_value = total_in if layout == snappy_amd.SINGLE else n
+        self.pre_clen = None
+        self.g_offs = None
+        if self.decode_only:  # the stream and its block index exist before the timed region
+            self.pre_clen = self.compress_all()
+            self.g_offs = torch.cat([p.offs[:-1] + p.out_off for p in self.pieces] +
+                                    [torch.tensor([self.pre_clen], dtype=torch.int64, device=dev)])
+
+    def compress_all(self) -> int:
+        o = 0
+        for p in self.pieces:
+            p.out_off = o
+            p.clen = self.codec.compress_ptr_ex(self.x.data_ptr() + p.off, p.n, self.chunk, self.layout, p.flags,
+                                                self.header_value, self.out.data_ptr() + o, p.offs.data_ptr())
+            o += p.clen
+        return o
+
+    def decompress_all(self, base_ptr=None) -> None:
+        """Decode every piece from the payload at base_ptr (default: this rank's own)."""
+        base_ptr = self.out.data_ptr() if base_ptr is None else base_ptr
+        if self.decode_only:
+            self.codec.decompress_ptr_ex(base_ptr, self.g_offs.data_ptr(), self.n, self.chunk, self.layout,
+                                         self.pieces[0].flags, self.header_value, self.back.data_ptr(), check=False)
+            return
+        for p in self.pieces:
+            self.codec.decompress_ptr_ex(base_ptr + p.out_off, p.offs.data_ptr(), p.n, self.chunk, self.layout,
+                                         p.flags, self.header_value, self.back.data_ptr() + p.off, check=False)
+
+    def verify(self) -> bool:
+        st = self.codec.decompress_status()
+        if st != 0:
+            return False
+        # in 1 GiB slices: torch.equal's temporaries stay small next to a 64 GiB shard
+        return all(bool(torch.equal(self.back[o:min(o + GiB, self.n)], self.x[o:min(o + GiB, self.n)]))
+                   for o in range(0, self.n, GiB))
+
+    def free(self):
+        for a in ("x", "out", "back", "g_offs"):
+            setattr(self, a, None)
+        for p in self.pieces:
+            p.offs = None
+        torch.cuda.empty_cache()
+
+
+def timed_steps(job: Job, steps: int, warmup: int, world: int, c1=None):
+    """Warm up, then time exactly `steps` steps between barrier + synchronize;
+    returns (elapsed seconds of this rank, clen, [k1 ms], [k3 ms], [k4 ms])."""
+    dev = job.dev
+
+    def step():
+        if job.decode_only:
+            job.decompress_all()
+            return job.pre_clen
+        clen = job.compress_all()
+        if c1 is not None:
+            c1(clen)
+        job.decompress_all()
+        return clen
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    k1, k3, k4 = [], [], []
+    clen = 0
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        clen = step()
+        a, b, c = job.codec.last_timings()
+        k1.append(a), k3.append(b), k4.append(c)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    return time.perf_counter() - t0, clen, k1, k3, k4
+
+
+def kernel_report(job: Job, clen: int, k1, k3, k4, pmc: dict) -> dict:
+    """Kernel times of the step's last launch (the last piece, or the one
+    decode), the dominant kernel's roofline and the per-path traffic."""
+    k1m, k3m, k4m = (float(np.mean(v)) for v in (k1, k3, k4))
+    lastp = job.pieces[-1]
+    comp_bytes = clen if job.decode_only else lastp.clen
+    kern_n = job.n if job.decode_only else lastp.n
+    # dominant kernel (longest average launch) and its algorithmic bytes per
+    # launch (SURVEY.md 8(d)): compress = N_in + N_out, decompress = N_comp + N_out
+    k1_name = "k1r_match_units" if job.chunk <= 32768 else "k1r_match_units64"
+    alg = kern_n + comp_bytes
+    cands = [(k1m, k1_name, alg), (k4m, "k4_decompress_units", alg)]
+    if job.decode_only:
+        cands = cands[1:]
+    dom_ms, dom_name, dom_bytes = max(cands)
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    traffic = pmc.get(dom_name)
+    roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "kernel": dom_name, "kernel_ms": round(dom_ms, 3), "algorithmic_bytes_per_launch": dom_bytes}
+    # counter bytes of each whole path (K1r + K3 + K2 write the compressed
+    # bytes; K4 alone decodes) beside the same path's algorithmic bytes
+    paths = {}
+    comp_k = [k1_name, "k3_scan", "k2_emit_units"]
+    if not job.decode_only and all(pmc.get(k) is not None for k in comp_k):
+        t = sum(pmc[k] for k in comp_k)
+        paths["compress"] = {"counter_bytes": t, "algorithmic_bytes": alg, "ratio": round(t / alg, 3),
+                             "kernels": comp_k}
+    if pmc.get("k4_decompress_units") is not None:
+        t = pmc["k4_decompress_units"] + (pmc.get("k4_decompress_back") or 0)
+        paths["decompress"] = {"counter_bytes": t, "algorithmic_bytes": alg, "ratio": round(t / alg, 3),
+                               "kernels": ["k4_decompress_units", "k4_decompress_back"]}
+    if paths:
+        roof["path_traffic"] = paths
+    return {
+        "roofline": roof,
+        "compress_MBps": None if job.decode_only else round(kern_n / ((k1m + k3m) * 1e-3) / 1e6, 1),
+        "decompress_MBps": round(kern_n / (k4m * 1e-3) / 1e6, 1),
+        # src/result.c:40 defines decompress speed over the compressed bytes
+        "decompress_MBps_ref_definition": round(comp_bytes / (k4m * 1e-3) / 1e6, 1),
+        "kernel_ms": {"k1_match": None if job.decode_only else round(k1m, 3),
+                      "k3_scan_k2_emit": None if job.decode_only else round(k3m, 3),
+                      "k4_decode": round(k4m, 3)},
+        "hbm_frac": {"compress_k1": None if job.decode_only else round(alg / (k1m * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                     "decompress_k4": round(alg / (k4m * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)},
+    }
+
+
+def sub_result(name: str, codec, dev, steps: int, warmup: int, piece_bytes: int, cpu: bool) -> dict:
+    """A compact single-GPU line for another BASELINE config (1 GiB, or the
+    ~10 GB stream of decode10g), with its own kernel times, roofline and a
+    CPU baseline on a 64 MiB sample of the same workload."""
+    n = DECODE10G_BYTES if name in DECODE_ONLY else GiB
+    t_gen = time.perf_counter()
+    job = Job(name, codec, dev, n, 0, n, n, piece_bytes)
+    t_gen = time.perf_counter() - t_gen
+    elapsed, clen, k1, k3, k4 = timed_steps(job, steps, warmup, 1)
+    ok = job.verify()
+    rep = kernel_report(job, clen, k1, k3, k4, load_pmc(pmc_path(name), name, job.n if job.decode_only
+                                                          else job.pieces[-1].n))
+    total_comp = clen
+    job.free()
+    res = {"workload": f"{name}: {n / GiB:.4g} GiB, {job.desc}", "value": round(n / (elapsed / steps) / 1e6, 1),
+           "unit": "MB/s", "steps": steps, "ms_per_step": round(elapsed / steps * 1e3, 3),
+           "ratio": round(n / total_comp, 4), "compress_MBps": rep["compress_MBps"],
+           "decompress_MBps": rep["decompress_MBps"], "kernel_ms": rep["kernel_ms"],
+           "roofline": {k: rep["roofline"][k] for k in ("kernel", "kernel_ms", "achieved", "frac", "traffic")},
+           "round_trip_ok": ok, "setup_s": round(t_gen, 1)}
+    if "path_traffic" in rep["roofline"]:
+        res["roofline"]["path_traffic"] = rep["roofline"]["path_traffic"]
+    if cpu:
+        kind, seed, layout, chunk, _ = WORKLOADS[name]
+        base, _ = cpu_baseline(kind, seed, chunk, layout, 64 << 20, name in DECODE_ONLY, all_cores=False)
+        res["cpu_baseline"] = base
+    return res
+
+
+def resolve_sizes(args, world: int, rank: int):
+    """(strong, total input bytes, this rank's offset, its bytes, the largest
+    rank's bytes).  N > 1 without size flags is configs[3] (64 GiB in total,
+    strong scaling); N = 1 without them configs[1] (1 GiB)."""
+    kind, seed, layout, chunk, desc = WORKLOADS[args.workload]
+    unit = chunk if layout == snappy_amd.STREAMS else 65536
+    total = args.total_bytes
+    if world > 1 and not args.weak and total == 0 and args.workload not in DECODE_ONLY:
+        total = CONFIG3_BYTES
+    if total > 0:
+        r_off, n = shard_range(total, world, rank, unit)
+        n_max = max(shard_range(total, world, r, unit)[1] for r in range(world))
+        return True, total, r_off, n, n_max
+    n = args.bytes_per_gpu
+    if args.workload in DECODE_ONLY and n == GiB and not args.keep_size:
+        n = DECODE10G_BYTES
+    return False, n * world, rank * n, n, n
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -278,8 +588,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     gloo = args.dist_backend == "gloo"
-    if world > 1:
+    # a process group also at N = 1 with --dist-world1 (the exchange code path
+    # over a 1-rank RCCL communicator: what a 1-GPU box can run of it)
+    use_dist = world > 1 or args.dist_world1
+    if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         # gloo: rehearsal of the multi-rank path (ranks may share a GPU)
         local = local % torch.cuda.device_count() if gloo else local
         torch.cuda.set_device(local)
@@ -289,48 +605,20 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+    dev = torch.device("cuda", local if use_dist else 0)
     cdev = torch.device("cpu") if gloo else dev  # where collective tensors live
 
-    kind, seed, layout, chunk, desc = WORKLOADS[args.workload]
     decode_only = args.workload in DECODE_ONLY
+    kind, seed, layout, chunk, desc = WORKLOADS[args.workload]
     unit = chunk if layout == snappy_amd.STREAMS else 65536
-    strong = args.total_bytes > 0
-    if strong:
-        total_in = args.total_bytes
-        r_off, n = shard_range(total_in, world, rank, unit)
-    else:
-        n = args.bytes_per_gpu
-        if decode_only and n == GiB and not args.keep_size:
-            n = DECODE10G_BYTES
-        total_in = n * world
-        r_off = rank * n
-    # the rank's range in HBM, generated on the host 1 GiB at a time
-    x = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
-    host = np.empty(min(max(n, 1), GiB), dtype=np.uint8)
-    for o in range(0, n, GiB):
-        m = min(GiB, n - o)
-        datagen.fill(host[:m], kind, seed, offset=r_off + o, threads=16)
-        x[o:o + m].copy_(torch.from_numpy(host[:m]))
-    del host
+    strong, total_in, r_off, n, n_max = resolve_sizes(args, world, rank)
     codec = snappy_amd.Codec(dev.index)
     codec.enable_timing(True)
     stream = torch.cuda.current_stream(dev)
     codec.set_stream(stream.cuda_stream)
-    units = codec.num_units(n, chunk, layout)
-    # pieces (unit-aligned) bound the K1r token scratch of one call
-    step_bytes = max(unit, (args.piece_bytes // unit) * unit)
-    pieces = []
-    for o in range(0, n, step_bytes):
-        flags = snappy_amd.NO_PREAMBLE if (layout == snappy_amd.SINGLE and (r_off + o) > 0) else 0
-        pieces.append(Piece(o, min(step_bytes, n - o), flags))
-    out = torch.empty(max(sum(codec.max_output(p.n, chunk, layout) for p in pieces), 16), dtype=torch.uint8,
-                      device=dev)
-    for p in pieces:
-        p.offs = torch.empty(codec.num_units(p.n, chunk, layout) + 1, dtype=torch.int64, device=dev)
-    back = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
-    # SINGLE layout: the stream's first piece carries the global preamble
-    header_value = total_in if layout == snappy_amd.SINGLE else n
+    t_setup = time.perf_counter()
+    job = Job(args.workload, codec, dev, n, r_off, total_in, n_max, args.piece_bytes)
+    t_setup = time.perf_counter() - t_setup
     sizes_t = torch.zeros(world, dtype=torch.int64, device=cdev)
 
     def allgather(dst, src):
@@ -342,62 +630,15 @@ def main():
         else:
             dist.all_gather_into_tensor(dst, src)
 
-    def compress_all():
-        o = 0
-        for p in pieces:
-            p.out_off = o
-            p.clen = codec.compress_ptr_ex(x.data_ptr() + p.off, p.n, chunk, layout, p.flags, header_value,
-                                           out.data_ptr() + o, p.offs.data_ptr())
-            o += p.clen
-        return o
+    def c1(clen):  # C1: shard sizes -> global stream offsets
+        allgather(sizes_t, torch.tensor([clen], dtype=torch.int64, device=cdev))
 
-    def decompress_all():
-        for p in pieces:
-            codec.decompress_ptr_ex(out.data_ptr() + p.out_off, p.offs.data_ptr(), p.n, chunk, layout, p.flags,
-                                    header_value, back.data_ptr() + p.off, check=False)
-
-    pre_clen = None
-    g_offs = None
-    g_flags = pieces[0].flags
-    if decode_only:  # the stream and its block index exist before the timed region
-        pre_clen = compress_all()
-        # one index over the whole rank stream (the pieces' indexes shifted to their payload offsets)
-        g_offs = torch.cat([p.offs[:-1] + p.out_off for p in pieces] +
-                           [torch.tensor([pre_clen], dtype=torch.int64, device=dev)])
-
-    def step():
-        if decode_only:
-            codec.decompress_ptr_ex(out.data_ptr(), g_offs.data_ptr(), n, chunk, layout, g_flags, header_value,
-                                    back.data_ptr(), check=False)
-            return pre_clen
-        clen = compress_all()
-        if world > 1:  # C1: shard sizes -> global stream offsets
-            mine = torch.tensor([clen], dtype=torch.int64, device=cdev)
-            allgather(sizes_t, mine)
-        decompress_all()
-        return clen
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    k1, k3, k4 = [], [], []
-    t0 = time.perf_counter()
-    clen = 0
-    for _ in range(args.steps):
-        clen = step()
-        a, b, c = codec.last_timings()
-        k1.append(a), k3.append(b), k4.append(c)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    st = codec.decompress_status()
-    ok = st == 0 and bool(torch.equal(back[:n], x[:n]))
-    if world > 1:
+    elapsed, clen, k1, k3, k4 = timed_steps(job, args.steps, args.warmup, world if use_dist else 1,
+                                            c1 if use_dist else None)
+    scratch_peak = codec.device_bytes()
+    torch_peak = torch.cuda.max_memory_allocated(dev)  # the buffers of the steps, before any check runs
+    ok = job.verify()
+    if use_dist:
         t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, bad = float(t[0]), float(t[1])
@@ -407,37 +648,31 @@ def main():
         total_comp = int(tot)
     else:
         total_comp = clen
+    mem_after_steps = torch.cuda.mem_get_info(dev)
 
     assemble = None
-    if world > 1 and not args.no_assemble:
-        assemble = exchange(out, clen, back, n, world, dev, cdev, gloo, allgather)
+    if use_dist and not args.no_assemble and not decode_only:
+        assemble = end_to_end(job, world, rank, args, cdev, gloo, allgather, total_in)
+        torch_peak = max(torch_peak, assemble.pop("torch_peak_bytes"))
         ok = ok and assemble["verified"]
+        if args.c3:
+            assemble["c3_decoded_allgather"] = gather_decoded(job, world, cdev, gloo, allgather)
+            ok = ok and assemble["c3_decoded_allgather"]["verified"]
 
-    hbm_gbps = hbm_copy_gbps(dev) if rank == 0 else None
     ms_step = elapsed / args.steps * 1e3
     value = total_in / (elapsed / args.steps) / 1e6
-    # kernel times are those of the step's last launch (the last piece, or the one decode)
-    k1m, k3m, k4m = (float(np.mean(v)) for v in (k1, k3, k4))
-    lastp = pieces[-1]
-    comp_bytes = clen if decode_only else lastp.clen
-    kern_n = n if decode_only else lastp.n
-    # dominant kernel (longest average launch) and its algorithmic bytes per
-    # launch: compress = N_in + N_out, decompress = N_comp + N_out
-    k1_name = "k1r_match_units" if chunk <= 32768 else "k1r_match_units64"
-    cands = [(k1m, k1_name, kern_n + comp_bytes), (k4m, "k4_decompress_units", comp_bytes + kern_n)]
-    if decode_only:
-        cands = cands[1:]
-    dom_ms, dom_name, dom_bytes = max(cands)
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    traffic = None
-    try:
-        pm = json.load(open(args.pmc))
-        if pm.get("workload") == args.workload and pm.get("bytes_per_gpu") == kern_n:
-            traffic = pm["kernels"].get(dom_name, {}).get("hbm_bytes")
-    except (OSError, ValueError, KeyError):
-        pass
+    pmc = load_pmc(args.pmc, args.workload, job.n if decode_only else job.pieces[-1].n)
+    rep = kernel_report(job, clen, k1, k3, k4, pmc)
+    plan = rank_plan(total_in if strong else n * world, world, unit, args.piece_bytes,
+                     exchange=world > 1 and not args.no_assemble, gather_decoded=args.c3)
+    used = mem_after_steps[1] - mem_after_steps[0]
+    rank_peak = torch_peak + scratch_peak
+    n_units = job.units
+    job.free()
 
+    line = None
     if rank == 0:
+        hbm_gbps = hbm_copy_gbps(dev)
         cpu = cpu_all = cpu_ref = e2e = None
         if world == 1 and not args.no_cpu_baseline:
             cpu, cpu_all = cpu_baseline(kind, seed, chunk, layout, min(args.cpu_sample_bytes, n), decode_only)
@@ -446,86 +681,163 @@ def main():
             e2e = host_end_to_end(kind, seed, min(n, 256 << 20))
         size_txt = (f"{total_in / GiB:.4g} GiB in total over {world} GPU(s)" if strong else
                     f"{n / GiB:.4g} GiB/GPU")
+        cfg_name = "configs[3]" if strong and args.workload == "text32k" else \
+            {"text32k": "configs[1]", "text64k": "configs[1] (64 KiB blocks)", "random": "configs[2]",
+             "repeat": "configs[2]", "decode10g": "configs[4]"}[args.workload]
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": f"{args.workload}: {size_txt}, {desc}; one step = "
-                                   + ("one decode of the stream" if decode_only else "compress + decompress round trip"),
+            "config": {"workload": f"{args.workload} ({cfg_name}): {size_txt}, {desc}; one step = "
+                                   + ("one decode of the stream" if decode_only else
+                                      "compress + decompress round trip" + (" + C1 size all-gather" if world > 1
+                                                                            else "")),
                        "bytes_per_gpu": n, "total_bytes": total_in, "chunk": chunk,
-                       "layout": "STREAMS" if layout else "SINGLE", "units_per_gpu": units,
-                       "pieces_per_gpu": len(pieces), "parallelism": f"dp{world} (block shards)"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "kernel": dom_name, "kernel_ms": round(dom_ms, 3),
-                         "algorithmic_bytes_per_launch": dom_bytes},
+                       "layout": "STREAMS" if layout else "SINGLE", "units_per_gpu": n_units,
+                       "pieces_per_gpu": len(job.pieces), "parallelism": f"dp{world} (block shards)"},
+            "roofline": rep["roofline"],
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
             "cpu_reference": cpu_ref,
             "ratio": round(total_in / total_comp, 4),
-            "compress_MBps": None if decode_only else round(kern_n / ((k1m + k3m) * 1e-3) / 1e6, 1),
-            "decompress_MBps": round(kern_n / (k4m * 1e-3) / 1e6, 1),
-            # src/result.c:40 defines decompress speed over the compressed bytes
-            "decompress_MBps_ref_definition": round(comp_bytes / (k4m * 1e-3) / 1e6, 1),
+            "compress_MBps": rep["compress_MBps"],
+            "decompress_MBps": rep["decompress_MBps"],
+            "decompress_MBps_ref_definition": rep["decompress_MBps_ref_definition"],
             "hbm_copy_GBps_measured": hbm_gbps,
             "host_end_to_end": e2e,
-            "kernel_ms": {"k1_match": None if decode_only else round(k1m, 3),
-                          "k3_scan_k2_emit": None if decode_only else round(k3m, 3),
-                          "k4_decode": round(k4m, 3)},
-            "hbm_frac": {"compress_k1": None if decode_only else
-                         round((kern_n + comp_bytes) / (k1m * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
-                         "decompress_k4": round((kern_n + comp_bytes) / (k4m * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)},
+            "kernel_ms": rep["kernel_ms"],
+            "hbm_frac": rep["hbm_frac"],
+            "memory": {"rank_peak_bytes": int(rank_peak), "torch_peak_bytes": int(torch_peak),
+                       "codec_scratch_bytes": int(scratch_peak), "device_bytes_in_use_after_steps": int(used),
+                       "planned_peak_bytes_per_rank": plan["peak"], "hbm_bytes": HBM_BYTES,
+                       "note": "rank_peak = torch allocator peak (shard, payload, decoded, indexes, C2 buffers) + "
+                               "codec scratch (hipMalloc'd by the library); plan = dist.rank_plan, worst case"},
+            "setup_s": round(t_setup, 1),
             "round_trip_ok": ok,
         }
         if assemble:
+            line["value_end_to_end"] = assemble.pop("value_end_to_end")
             line["exchange"] = assemble
+    if rank == 0 and world == 1 and not args.no_sub and args.workload == "text32k" and not strong:
+        subs = {}
+        sub_steps, sub_warm = max(1, min(args.steps, 10)), min(args.warmup, 2)
+        for w in SUB_WORKLOADS:
+            codec.trim()
+            subs[w] = sub_result(w, codec, dev, sub_steps, sub_warm, args.piece_bytes, not args.no_cpu_baseline)
+            ok = ok and subs[w]["round_trip_ok"]
+        line["configs"] = subs
+        if not args.no_host_e2e:
+            codec.trim()
+            fa = host_file_api(args.file_api_bytes)
+            line["host_file_api"] = fa
+            ok = ok and fa["round_trip_ok"]
+        line["round_trip_ok"] = ok
+    if line is not None:
         print(json.dumps(line), flush=True)
     codec.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
     if not ok:
         sys.exit(3)
 
 
-def exchange(out, clen, back, n, world, dev, cdev, gloo, allgather) -> dict:
-    """C2: every rank receives the whole compressed stream (padded all-gather:
-    RCCL has no all-gatherv); C3: every rank receives the whole decoded output.
-    Timed separately from the steps (max over ranks), verified with per-shard
-    checksums."""
-    res = {}
-    sizes = torch.zeros(2 * world, dtype=torch.int64, device=cdev)
-    allgather(sizes, torch.tensor([clen, n], dtype=torch.int64, device=cdev))
-    sizes = sizes.view(world, 2).cpu()
-    mx, mn = int(sizes[:, 0].max()), int(sizes[:, 1].max())  # shards differ (strong scaling): pad
-    sums = torch.zeros(2 * world, dtype=torch.int64, device=cdev)
-    allgather(sums, torch.tensor([checksum(out[:clen]), checksum(back[:n])], dtype=torch.int64, device=cdev))
-    pad = torch.zeros(mx, dtype=torch.uint8, device=cdev)
-    pad[:clen] = out[:clen].to(cdev)
-    full_c = torch.empty(world * mx, dtype=torch.uint8, device=cdev)
-    src_d = torch.zeros(mn, dtype=torch.uint8, device=cdev)
-    src_d[:n] = back[:n].to(cdev)
-    full_d = torch.empty(world * mn, dtype=torch.uint8, device=cdev)
-    for name, dst, src in (("c2_stream_allgather", full_c, pad), ("c3_decoded_allgather", full_d, src_d)):
-        allgather(dst, src)  # warm-up
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        t0 = time.perf_counter()
-        allgather(dst, src)
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=cdev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t = float(tt)
-        res[name] = {"ms": round(t * 1e3, 3), "bytes_per_rank_out": int(dst.numel()),
-                     "GBps_per_rank_in": round((world - 1) / world * dst.numel() / t / 1e9, 2)}
-    full_c, full_d = full_c.to(dev), full_d.to(dev)
-    good = True
+def end_to_end(job: Job, world: int, rank: int, args, cdev, gloo, allgather, total_in: int) -> dict:
+    """The whole job as one pipeline, timed over --e2e-steps steps (max over
+    ranks): compress the shard, C1 (size all-gather -> every shard's offset),
+    C2 (all-gather of the payloads padded to the largest: RCCL has no
+    all-gatherv), compaction of the padded gather into the contiguous stream
+    every rank then holds (byte-identical to a 1-GPU stream for SINGLE), and
+    decompress of this rank's blocks out of that stream.  Verified afterwards:
+    per-shard checksums of the reassembled stream and the round trip."""
+    dev = job.dev
+    sizes = torch.zeros(world, dtype=torch.int64, device=cdev)
+    state = {"full": None, "stream": None, "mx": 0}
+
+    def step():
+        clen = job.compress_all()
+        allgather(sizes, torch.tensor([clen], dtype=torch.int64, device=cdev))  # C1
+        sz = [int(v) for v in sizes.cpu()]
+        mx = max(max(sz), 1)
+        if state["full"] is None or state["full"].numel() < world * mx:
+            state["full"] = None
+            state["stream"] = None
+            torch.cuda.empty_cache()
+            state["full"] = torch.empty(world * mx, dtype=torch.uint8, device=cdev)
+            state["stream"] = torch.empty(max(sum(sz), 1), dtype=torch.uint8, device=dev)
+        full, stream = state["full"], state["stream"]
+        state["mx"] = mx
+        if gloo:
+            allgather(full[:world * mx], job.out[:mx].to(cdev))
+        else:
+            allgather(full[:world * mx], job.out[:mx])  # C2 (job.out holds >= mx bytes on every rank)
+        offs = np.concatenate([[0], np.cumsum(sz)])
+        for r in range(world):  # compaction: shard r from r * mx to its stream offset
+            stream[offs[r]:offs[r] + sz[r]].copy_(full[r * mx:r * mx + sz[r]], non_blocking=True)
+        job.decompress_all(stream.data_ptr() + int(offs[rank]))
+        return sz
+
+    step()  # untimed: allocates the gather buffers
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    steps = max(1, args.e2e_steps)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sz = step()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=cdev)
+    torch_peak = torch.cuda.max_memory_allocated(dev)  # before the checks' temporaries
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    t = float(tt) / steps
+    ok = job.verify()
+    # per-shard checksums: each rank's own payload against its slice of every rank's stream
+    mine = torch.tensor([checksum(job.out[:sz[rank]])], dtype=torch.int64, device=cdev)
+    sums = torch.zeros(world, dtype=torch.int64, device=cdev)
+    allgather(sums, mine)
+    offs = np.concatenate([[0], np.cumsum(sz)])
+    stream = state["stream"]
     for r in range(world):
-        good &= checksum(full_c[r * mx: r * mx + int(sizes[r, 0])]) == int(sums[2 * r])
-        good &= checksum(full_d[r * mn: r * mn + int(sizes[r, 1])]) == int(sums[2 * r + 1])
-    res["stream_bytes"] = int(sizes[:, 0].sum())
-    res["verified"] = bool(good)
+        ok &= checksum(stream[offs[r]:offs[r] + sz[r]]) == int(sums[r])
+    flag = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=cdev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    mx = state["mx"]
+    res = {"value_end_to_end": round(total_in / t / 1e6, 1),
+           "end_to_end_ms_per_step": round(t * 1e3, 3), "end_to_end_steps": steps,
+           "end_to_end_step": "compress + C1 + C2 padded all-gather + compaction + decompress from the stream",
+           "stream_bytes": int(sum(sz)), "c2_padded_bytes_per_rank_out": world * mx,
+           "backend": "gloo" if gloo else "nccl (RCCL)", "verified": float(flag) == 0.0,
+           "torch_peak_bytes": torch_peak}
+    state["full"] = state["stream"] = None
+    torch.cuda.empty_cache()
     return res
+
+
+def gather_decoded(job: Job, world: int, cdev, gloo, allgather) -> dict:
+    """C3 (opt-in): every rank receives every rank's decoded shard (padded to
+    the largest).  The codec scratch and the input are released first, so
+    this phase fits HBM at 64 GiB (dist.rank_plan)."""
+    dev = job.dev
+    job.codec.trim()
+    n, m = job.n, job.back.numel()
+    mine = torch.tensor([checksum(job.back[:n]), n], dtype=torch.int64, device=cdev)
+    info = torch.zeros(2 * world, dtype=torch.int64, device=cdev)
+    allgather(info, mine)
+    info = info.view(world, 2).cpu()
+    full = torch.empty(world * m, dtype=torch.uint8, device=cdev)
+    src = job.back if not gloo else job.back.to(cdev)
+    allgather(full, src)  # warm-up
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    allgather(full, src)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=cdev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    good = all(checksum(full[r * m:r * m + int(info[r, 1])]) == int(info[r, 0]) for r in range(world))
+    t = float(tt)
+    return {"ms": round(t * 1e3, 3), "bytes_per_rank_out": world * m,
+            "GBps_per_rank_in": round((world - 1) / world * world * m / t / 1e9, 2), "verified": bool(good)}
 
 
 if __name__ == "__main__":

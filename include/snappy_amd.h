@@ -94,6 +94,15 @@ void snappy_amd_destroy(snappy_amd_ctx *ctx);
 int snappy_amd_set_stream(snappy_amd_ctx *ctx, void *hip_stream);
 void *snappy_amd_get_stream(snappy_amd_ctx *ctx);
 
+/* Device bytes the context holds as scratch (token lists, segment records,
+ * status words, staging of the host-buffer path, index scratch); it grows to
+ * the largest call made and is kept. */
+size_t snappy_amd_device_bytes(snappy_amd_ctx *ctx);
+/* Release the scratch above (synchronises the context stream); the next call
+ * allocates again.  Used to make room in HBM between phases (bench.py frees
+ * the compressor's token lists before the all-gather of the shards). */
+int snappy_amd_trim(snappy_amd_ctx *ctx);
+
 /* Number of units (blocks or streams) for n bytes in a layout. */
 size_t snappy_amd_num_units(size_t n, uint32_t chunk, int layout);
 /* Capacity d_out must have for compress_device. */
@@ -152,6 +161,8 @@ int snappy_amd_decompress_device_ex(snappy_amd_ctx *ctx, const void *d_comp, con
 /* Build the block index of a SINGLE-layout stream already in HBM (e.g. a
  * file produced by the reference or another encoder): d_offsets gets
  * ceil(N/65536)+1 entries (format above), *n_out the declared length N.
+ * max_units = the entries d_offsets can hold (SNAPPY_AMD_ERR_CAPACITY if the
+ * stream needs more).
  * SNAPPY_AMD_ERR_UNSUPPORTED only if a straddling element starts past 2^40
  * bytes or covers a boundary more than 2^24 - 1 bytes after its start. */
 int snappy_amd_index_device(snappy_amd_ctx *ctx, const void *d_comp, size_t clen, uint64_t *d_offsets,

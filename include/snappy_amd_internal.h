@@ -26,6 +26,15 @@ int snappy_amd_host_decompress_idx(const uint8_t *in, size_t n, const uint64_t *
  * (varint(header_value) ++ blocks) to fout, and (fidx != NULL) the sidecar
  * index of snappy_amd.h to fidx; *bytes_in = bytes read. */
 int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, FILE *fidx, uint64_t *bytes_in);
+/* Pipelined snappy_decompress(): fin (a regular file, from its current
+ * position to EOF) is read in 64 MiB chunks by several threads into pinned
+ * staging and copied to HBM while the next chunk is read; the block index is
+ * the sidecar's (idx/count, checked) or built on the GPU; the decoded bytes
+ * come back in 64 MiB chunks written (positional writes when fout is a
+ * regular file, fwrite otherwise) while the next chunk is copied down.
+ * SNAPPY_AMD_ERR_UNSUPPORTED if fin is not a regular file (the caller then
+ * reads it whole and uses snappy_amd_host_decompress[_idx]). */
+int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count, FILE *fout);
 #ifdef __cplusplus
 }
 #endif

@@ -7,7 +7,13 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
+#include <fcntl.h>
 #include <mutex>
+#include <sys/stat.h>
+#include <thread>
+#include <unistd.h>
+#include <vector>
 
 #include "snappy_amd.h"
 #include "snappy_amd_internal.h"
@@ -55,7 +61,10 @@ static int grow(void **ptr, size_t *cap, size_t need)
     if (*ptr) (void)hipFree(*ptr);
     *ptr = nullptr;
     *cap = 0;
-    size_t want = need + need / 8 + 4096;
+    // slack for slowly growing calls, capped: a 16 GiB piece's token scratch
+    // must not carry 4 GB of slack (bench.py's per-rank memory plan counts it)
+    const size_t slack = need / 8 < ((size_t)64 << 20) ? need / 8 : ((size_t)64 << 20);
+    size_t want = need + slack + 4096;
     if (hipMalloc(ptr, want) != hipSuccess) { *ptr = nullptr; return SNAPPY_AMD_ERR_DEVICE; }
     *cap = want;
     return SNAPPY_AMD_OK;
@@ -122,6 +131,31 @@ void snappy_amd_destroy(snappy_amd_ctx *c)
     for (int i = 0; i < 5; i++) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
+}
+
+size_t snappy_amd_device_bytes(snappy_amd_ctx *c)
+{
+    if (!c) return 0;
+    return c->sizes_cap + c->tokens_cap + c->ntok_cap + c->seg_off_cap + c->status_cap + c->d_a_cap + c->d_b_cap +
+           c->d_idx_cap + c->k5buf_cap + c->k5copy_cap + 128;
+}
+
+int snappy_amd_trim(snappy_amd_ctx *c)
+{
+    if (!c) return SNAPPY_AMD_ERR_ARG;
+    HIP_OK(hipSetDevice(c->device));
+    if (c->stream) HIP_OK(hipStreamSynchronize(c->stream));
+    struct { void **p; size_t *cap; } bufs[] = {
+        {reinterpret_cast<void **>(&c->tokens), &c->tokens_cap}, {reinterpret_cast<void **>(&c->seg_off), &c->seg_off_cap},
+        {reinterpret_cast<void **>(&c->d_a), &c->d_a_cap}, {reinterpret_cast<void **>(&c->d_b), &c->d_b_cap},
+        {reinterpret_cast<void **>(&c->d_idx), &c->d_idx_cap}, {reinterpret_cast<void **>(&c->k5buf), &c->k5buf_cap},
+        {reinterpret_cast<void **>(&c->k5copy), &c->k5copy_cap}};
+    for (auto &b : bufs) {
+        if (*b.p) (void)hipFree(*b.p);
+        *b.p = nullptr;
+        *b.cap = 0;
+    }
+    return SNAPPY_AMD_OK;
 }
 
 int snappy_amd_set_stream(snappy_amd_ctx *c, void *s)
@@ -479,6 +513,97 @@ size_t read_full(FILE *f, uint8_t *b, size_t cap)
     return n;
 }
 
+// Threads copying file chunks between the page cache and pinned staging
+// (SNAPPY_AMD_IO_THREADS, default 8): one stdio thread moves a few GB/s, the
+// GPU path tens.
+int io_threads()
+{
+    static int t = 0;
+    if (!t) {
+        t = 8;
+        if (const char *e = getenv("SNAPPY_AMD_IO_THREADS")) t = atoi(e);
+        if (t < 1) t = 1;
+        if (t > 64) t = 64;
+    }
+    return t;
+}
+
+// pread/pwrite of [off, off + len) split over io_threads() threads in 1 MiB
+// aligned parts; returns the bytes moved (short only at EOF or on error)
+size_t par_io(int fd, uint8_t *buf, size_t len, uint64_t off, bool wr)
+{
+    const int nt = len >= ((size_t)4 << 20) ? io_threads() : 1;
+    const size_t per = ((len / nt) + (1 << 20) - 1) & ~(((size_t)1 << 20) - 1);
+    std::vector<size_t> done(nt, 0);
+    auto part = [&](int t) {
+        const size_t a = std::min(len, per * t), b = std::min(len, per * (t + 1));
+        size_t x = a;
+        while (x < b) {
+            const ssize_t r = wr ? pwrite(fd, buf + x, b - x, (off_t)(off + x)) : pread(fd, buf + x, b - x, (off_t)(off + x));
+            if (r <= 0) break;
+            x += (size_t)r;
+        }
+        done[t] = x - a;
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; t++) th.emplace_back(part, t);
+    part(0);
+    for (auto &x : th) x.join();
+    size_t tot = 0;  // the contiguous prefix moved (a short part ends it)
+    for (int t = 0; t < nt; t++) {
+        const size_t a = std::min(len, per * t), b = std::min(len, per * (t + 1));
+        tot += done[t];
+        if (done[t] != b - a) break;
+    }
+    return tot;
+}
+
+// A FILE* used from its current position: positional multi-threaded I/O on a
+// regular file (the stdio buffer is flushed / skipped; finish() leaves the
+// FILE* where the stdio calls would have), plain fread / fwrite otherwise
+// (pipes, terminals, files opened for append).
+struct IoFile {
+    FILE *f = nullptr;
+    int fd = -1;
+    bool pos_io = false;
+    uint64_t pos = 0;
+    bool open(FILE *file, bool wr)
+    {
+        f = file;
+        if (wr && fflush(f) != 0) return false;
+        fd = fileno(f);
+        struct stat st;
+        const off_t p = ftello(f);
+        pos_io = fd >= 0 && p >= 0 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode) &&
+                 !(wr && (fcntl(fd, F_GETFL) & O_APPEND));
+        pos = pos_io ? (uint64_t)p : 0;
+        return true;
+    }
+    uint64_t remaining() const  // bytes to EOF (positional readers only)
+    {
+        struct stat st;
+        if (!pos_io || fstat(fd, &st) != 0) return 0;
+        return (uint64_t)st.st_size > pos ? (uint64_t)st.st_size - pos : 0;
+    }
+    size_t read(uint8_t *b, size_t cap)
+    {
+        if (!pos_io) return read_full(f, b, cap);
+        const size_t got = par_io(fd, b, cap, pos, false);
+        pos += got;
+        return got;
+    }
+    bool write(const uint8_t *b, size_t len)
+    {
+        if (!len) return true;
+        if (!pos_io) return fwrite(b, 1, len, f) == len;
+        const size_t put = par_io(fd, const_cast<uint8_t *>(b), len, pos, true);
+        pos += put;
+        return put == len;
+    }
+    bool error() const { return !pos_io && ferror(f); }
+    bool finish() { return !pos_io || fseeko(f, (off_t)pos, SEEK_SET) == 0; }
+};
+
 void slot_free(StreamSlot &s)
 {
     for (void *h : {(void *)s.h_in, (void *)s.h_out, (void *)s.h_idx})
@@ -512,7 +637,7 @@ int slot_init(StreamSlot &s, int device)
 // finish slot s: its compressed size is in s.c->h_total once its stream drains.
 // With a sidecar file, the chunk's block index goes out too, shifted by the
 // stream bytes written before it (*base); the stream-end entry is left to the caller.
-int slot_drain(StreamSlot &s, FILE *fout, FILE *fidx, uint64_t *base)
+int slot_drain(StreamSlot &s, IoFile &fout, FILE *fidx, uint64_t *base)
 {
     if (!s.busy) return SNAPPY_AMD_OK;
     s.busy = false;
@@ -522,7 +647,7 @@ int slot_drain(StreamSlot &s, FILE *fout, FILE *fidx, uint64_t *base)
     HIP_OK(hipMemcpyAsync(s.h_out, s.d_out, len, hipMemcpyDeviceToHost, s.c->stream));
     if (fidx) HIP_OK(hipMemcpyAsync(s.h_idx, s.d_idx, units * sizeof(uint64_t), hipMemcpyDeviceToHost, s.c->stream));
     HIP_OK(hipStreamSynchronize(s.c->stream));
-    if (len && fwrite(s.h_out, 1, len, fout) != len) return SNAPPY_AMD_ERR_IO;
+    if (!fout.write(s.h_out, len)) return SNAPPY_AMD_ERR_IO;
     if (fidx) {
         for (size_t i = 0; i < units; i++) s.h_idx[i] += *base;
         if (fwrite(s.h_idx, sizeof(uint64_t), units, fidx) != units) return SNAPPY_AMD_ERR_IO;
@@ -545,6 +670,8 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
     }
     int dev = 0;
     if (const char *e = getenv("SNAPPY_AMD_DEVICE")) dev = atoi(e);
+    IoFile in, out;
+    if (!in.open(fin, false) || !out.open(fout, true)) return SNAPPY_AMD_ERR_IO;
     int rc;
     for (auto &s : g_slots) {
         if ((rc = slot_init(s, dev))) return rc;
@@ -555,8 +682,8 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
     }
     HIP_OK(hipSetDevice(dev));
     uint64_t total_in = 0;
-    size_t n = read_full(fin, g_slots[0].h_in, kStreamChunk);
-    if (ferror(fin)) return SNAPPY_AMD_ERR_IO;
+    size_t n = in.read(g_slots[0].h_in, kStreamChunk);
+    if (in.error()) return SNAPPY_AMD_ERR_IO;
     for (uint32_t k = 0; n > 0; k++) {
         StreamSlot &s = g_slots[k & 1];
         StreamSlot &o = g_slots[(k + 1) & 1];
@@ -570,14 +697,15 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
         s.busy = true;
         // chunk k-1 out while chunk k runs, then chunk k+1 in (its slot is free
         // once chunk k-1 drained)
-        if ((rc = slot_drain(o, fout, fidx, &base))) return rc;
-        n = read_full(fin, o.h_in, kStreamChunk);
-        if (ferror(fin)) return SNAPPY_AMD_ERR_IO;
+        if ((rc = slot_drain(o, out, fidx, &base))) return rc;
+        n = in.read(o.h_in, kStreamChunk);
+        if (in.error()) return SNAPPY_AMD_ERR_IO;
     }
     // the slots drain in chunk order: the one holding the last chunk goes last
     const uint32_t last = total_in ? (uint32_t)(((total_in + kStreamChunk - 1) / kStreamChunk - 1) & 1) : 0;
-    if ((rc = slot_drain(g_slots[last ^ 1], fout, fidx, &base))) return rc;
-    if ((rc = slot_drain(g_slots[last], fout, fidx, &base))) return rc;
+    if ((rc = slot_drain(g_slots[last ^ 1], out, fidx, &base))) return rc;
+    if ((rc = slot_drain(g_slots[last], out, fidx, &base))) return rc;
+    if (!in.finish() || !out.finish()) return SNAPPY_AMD_ERR_IO;
     if (fidx) {
         // the stream's preamble says header_value; an index is only valid for a
         // stream whose preamble is the length actually compressed
@@ -639,6 +767,102 @@ int snappy_amd_host_decompress_idx(const uint8_t *in, size_t n, const uint64_t *
     HIP_OK(hipStreamSynchronize(c->stream));
     *out_len = (size_t)N;
     return SNAPPY_AMD_OK;
+}
+
+// pinned staging of the FILE* decoder: 3 chunks in rotation (one being
+// filled or drained by the host threads while the copy engine moves another)
+namespace {
+struct DecStage {
+    uint8_t *h[3] = {};
+    hipEvent_t ev[3] = {};
+    bool ready = false;
+};
+DecStage g_dec;
+
+int dec_stage_init()
+{
+    if (g_dec.ready) return SNAPPY_AMD_OK;
+    for (int i = 0; i < 3; i++) {
+        if (hipHostMalloc(&g_dec.h[i], kStreamChunk, hipHostMallocDefault) != hipSuccess ||
+            hipEventCreateWithFlags(&g_dec.ev[i], hipEventDisableTiming) != hipSuccess) {
+            for (int j = 0; j <= i; j++) {
+                if (g_dec.h[j]) (void)hipHostFree(g_dec.h[j]);
+                if (g_dec.ev[j]) (void)hipEventDestroy(g_dec.ev[j]);
+                g_dec.h[j] = nullptr;
+                g_dec.ev[j] = nullptr;
+            }
+            return SNAPPY_AMD_ERR_DEVICE;
+        }
+    }
+    g_dec.ready = true;
+    return SNAPPY_AMD_OK;
+}
+}  // namespace
+
+int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count, FILE *fout)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!fin || !fout) return SNAPPY_AMD_ERR_ARG;
+    IoFile in, out;
+    if (!in.open(fin, false) || !in.pos_io) return SNAPPY_AMD_ERR_UNSUPPORTED;
+    const uint64_t n = in.remaining();
+    if (n == 0) return in.finish() ? SNAPPY_AMD_OK : SNAPPY_AMD_ERR_IO;  // nothing to decode, nothing written
+    snappy_amd_ctx *c;
+    int rc = global_ctx(&c);
+    if (rc) return rc;
+    if ((rc = dec_stage_init())) return rc;
+    HIP_OK(hipSetDevice(c->device));
+    if ((rc = grow(reinterpret_cast<void **>(&c->d_a), &c->d_a_cap, n + 16))) return rc;
+    // (1) file -> pinned chunk k % 3 (host threads) -> HBM (copy engine), the
+    // next chunk read while this one is copied
+    uint64_t N = 0;
+    const uint64_t nch = (n + kStreamChunk - 1) / kStreamChunk;
+    for (uint64_t k = 0; k < nch; k++) {
+        const int s = (int)(k % 3);
+        if (k >= 3) HIP_OK(hipEventSynchronize(g_dec.ev[s]));
+        const size_t m = (size_t)std::min<uint64_t>(kStreamChunk, n - k * kStreamChunk);
+        if (in.read(g_dec.h[s], m) != m) return SNAPPY_AMD_ERR_IO;
+        if (k == 0 && snappy_varint_decode(g_dec.h[0], m, &N) == 0) return SNAPPY_AMD_ERR_HEADER;
+        HIP_OK(hipMemcpyAsync(c->d_a + k * kStreamChunk, g_dec.h[s], m, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(hipEventRecord(g_dec.ev[s], c->stream));
+    }
+    if (!in.finish()) return SNAPPY_AMD_ERR_IO;
+    // (2) block index (sidecar, checked, or the GPU index pass) and decode
+    const uint64_t units = (N + SNAPPY_AMD_BLOCK - 1) / SNAPPY_AMD_BLOCK;
+    if ((rc = grow(reinterpret_cast<void **>(&c->d_b), &c->d_b_cap, N + 16))) return rc;
+    if ((rc = grow(reinterpret_cast<void **>(&c->d_idx), &c->d_idx_cap, (units + 2) * sizeof(uint64_t)))) return rc;
+    if (idx) {
+        const uint64_t off_mask = (1ull << SNAPPY_AMD_IDX_OFFSET_BITS) - 1;
+        if (count != units + 1 || (idx[units] & off_mask) != n) return SNAPPY_AMD_ERR_INDEX;
+        for (uint64_t i = 0; i < units; i++)
+            if ((idx[i] & off_mask) > (idx[i + 1] & off_mask)) return SNAPPY_AMD_ERR_INDEX;
+        HIP_OK(hipMemcpyAsync(c->d_idx, idx, count * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    } else {
+        size_t got = 0;
+        if ((rc = snappy_amd_index_device(c, c->d_a, n, c->d_idx, units + 1, &got))) return rc;
+    }
+    if (N == 0) return SNAPPY_AMD_OK;
+    if ((rc = snappy_amd_decompress_device(c, c->d_a, c->d_idx, (size_t)N, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE,
+                                           c->d_b)))
+        return rc;
+    // (3) HBM -> pinned chunk (copy engine) -> file (host threads), the next
+    // chunk copied down while this one is written
+    if (!out.open(fout, true)) return SNAPPY_AMD_ERR_IO;
+    const uint64_t och = (N + kStreamChunk - 1) / kStreamChunk;
+    auto down = [&](uint64_t k) -> int {
+        const size_t m = (size_t)std::min<uint64_t>(kStreamChunk, N - k * kStreamChunk);
+        HIP_OK(hipMemcpyAsync(g_dec.h[k % 3], c->d_b + k * kStreamChunk, m, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipEventRecord(g_dec.ev[k % 3], c->stream));
+        return SNAPPY_AMD_OK;
+    };
+    if ((rc = down(0))) return rc;
+    for (uint64_t k = 0; k < och; k++) {
+        if (k + 1 < och && (rc = down(k + 1))) return rc;
+        HIP_OK(hipEventSynchronize(g_dec.ev[k % 3]));
+        const size_t m = (size_t)std::min<uint64_t>(kStreamChunk, N - k * kStreamChunk);
+        if (!out.write(g_dec.h[k % 3], m)) return SNAPPY_AMD_ERR_IO;
+    }
+    return out.finish() ? SNAPPY_AMD_OK : SNAPPY_AMD_ERR_IO;
 }
 
 }  // extern "C"

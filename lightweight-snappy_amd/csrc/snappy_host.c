@@ -125,8 +125,20 @@ static int decompress_file(FILE *file_input, FILE *idx, FILE *file_decompressed,
     uint8_t *in = NULL, *out = NULL;
     uint64_t *ent = NULL;
     size_t n = 0, len = 0, count = 0;
-    int rc = (file_input && file_decompressed) ? slurp(file_input, &in, &n) : SNAPPY_AMD_ERR_ARG;
+    int rc = (file_input && file_decompressed) ? SNAPPY_AMD_OK : SNAPPY_AMD_ERR_ARG;
     if (rc == SNAPPY_AMD_OK && idx) rc = read_index(idx, &ent, &count);
+    /* a regular file: the pipelined decoder (chunked reads overlapped with the
+     * copies to HBM, chunked copies back overlapped with the writes) */
+    if (rc == SNAPPY_AMD_OK) {
+        rc = snappy_amd_host_decompress_file(file_input, ent, count, file_decompressed);
+        if (rc != SNAPPY_AMD_ERR_UNSUPPORTED) {
+            free(ent);
+            g_last_status = rc;
+            if (rc != SNAPPY_AMD_OK) fprintf(stderr, "%s: error %d\n", what, rc);
+            return rc;
+        }
+        rc = slurp(file_input, &in, &n); /* a pipe: read it whole (the reference's decoder needs fseek anyway) */
+    }
     if (rc == SNAPPY_AMD_OK && n > 0) {
         uint64_t N = 0;
         rc = snappy_uncompressed_length(in, n, &N);

@@ -1984,7 +1984,7 @@ __global__ __launch_bounds__(64) void k5_index_stream(const uint8_t *__restrict_
     }
     if (!done) st = SNAPPY_ST_HEADER;
     const uint64_t units = (N + SNAPPY_BLOCK - 1) / SNAPPY_BLOCK;
-    if (st == SNAPPY_ST_OK && units > max_units) st = SNAPPY_ST_CAPACITY;
+    if (st == SNAPPY_ST_OK && units >= max_units) st = SNAPPY_ST_CAPACITY;  // units + 1 entries needed
     uint64_t op = 0, unit = 0;
     if (st == SNAPPY_ST_OK && lane == 0 && units) offsets[0] = 0;
     unit = 1;
@@ -2603,7 +2603,7 @@ __global__ __launch_bounds__(64) void k5d_result(uint32_t nchunks, const int32_t
     int64_t st = result[0];
     const uint64_t N = (uint64_t)result[1];
     const uint64_t units = (N + SNAPPY_BLOCK - 1) / SNAPPY_BLOCK;
-    if (st == SNAPPY_ST_OK && units > max_units) st = SNAPPY_ST_CAPACITY;
+    if (st == SNAPPY_ST_OK && units >= max_units) st = SNAPPY_ST_CAPACITY;  // units + 1 entries needed
     for (uint32_t cb = 0; st == SNAPPY_ST_OK && cb < nchunks; cb += 64) {
         const int32_t v = cb + lane < nchunks ? cst[cb + lane] : 0;
         const uint64_t m = __ballot(v != SNAPPY_ST_OK);

@@ -29,6 +29,71 @@ def shard_range(n_total: int, world: int, rank: int, unit: int) -> Tuple[int, in
     return off, max(0, min(n_total, u1 * unit) - off)
 
 
+BLOCK = 65536
+GiB = 1 << 30
+HBM_BYTES = 288 * 10**9  # MI355X HBM3E, 288 GB (MI355X_MICROARCH.md; the spec figure, the smaller reading)
+K2_SEG = 256              # csrc/snappy_kernels.h SNAPPY_K2_SEG
+
+
+def max_output(n: int, unit: int) -> int:
+    """snappy_amd_max_output (csrc/snappy_device.hip): worst-case payload bytes."""
+    units = (n + unit - 1) // unit
+    return n + units * (unit // 32 + 32) + 16
+
+
+def _grown(need: int) -> int:
+    """Bytes grow() in csrc/snappy_device.hip allocates for `need`."""
+    return need + min(need // 8, 64 << 20) + 4096
+
+
+def pieces_of(n: int, unit: int, piece_bytes: int) -> List[int]:
+    """Sizes of the unit-aligned pieces bench.py compresses a rank's range in."""
+    step = max(unit, (piece_bytes // unit) * unit)
+    return [min(step, n - o) for o in range(0, n, step)]
+
+
+def rank_plan(total: int, world: int, unit: int, piece_bytes: int, exchange: bool = True,
+              gather_decoded: bool = False) -> dict:
+    """Peak device bytes of one bench.py rank (the largest shard) for a job of
+    `total` input bytes sharded over `world` ranks, worst case (incompressible
+    data: every payload at its snappy_amd_max_output bound).
+
+    Resident through the run: the shard (x), its payload (out, sized for the
+    largest shard so the C2 all-gather can send equal counts), the decoded
+    shard (back), the per-piece block indexes and the codec's scratch for the
+    largest piece (K1r token lists + escapes, token counts, unit sizes, K2
+    segment records, K4 status words).  With `exchange` (world > 1): C2's
+    padded all-gather buffer (world x payload) and the reassembled stream.
+    `gather_decoded` (C3, opt-in) runs after the codec scratch and C2 buffers
+    are released: every rank then also holds world x the largest shard."""
+    shard = max(shard_range(total, world, r, unit)[1] for r in range(world))
+    ps = pieces_of(shard, unit, piece_bytes)
+    big = max(ps) if ps else 0
+    units_big = (big + unit - 1) // unit
+    tok_cap = unit // 4 + 2
+    segs = (tok_cap + K2_SEG - 1) // K2_SEG
+    out_cap = sum(max_output(p, unit) for p in ps)
+    plan = {
+        "shard_x": shard,
+        "payload_out": out_cap,
+        "decoded_back": shard,
+        "block_indexes": sum(((p + unit - 1) // unit + 1) * 8 for p in ps),
+        "scratch_tokens": _grown(units_big * tok_cap * 8 + units_big * 32),
+        "scratch_counts_sizes": 2 * _grown(units_big * 4),
+        "scratch_segments": _grown(units_big * segs * 8),
+        "scratch_status": _grown((units_big + 2) * 4),
+    }
+    if exchange and world > 1:
+        plan["c2_gather_buffer"] = world * out_cap
+        plan["c2_stream"] = world * out_cap
+    plan["peak"] = sum(plan.values())
+    if gather_decoded and world > 1:
+        c3 = plan["shard_x"] + plan["payload_out"] + plan["decoded_back"] + plan["block_indexes"] + world * shard
+        plan["c3_phase_peak"] = c3
+        plan["peak"] = max(plan["peak"], c3)
+    return plan
+
+
 def exchange_sizes(local_size: int, device, group=None) -> List[int]:
     """C1: every rank learns every shard's compressed size."""
     world = dist.get_world_size(group)

@@ -76,6 +76,8 @@ _SIGS = {
     "snappy_amd_destroy": (None, [_c.c_void_p]),
     "snappy_amd_set_stream": (_c.c_int, [_c.c_void_p, _c.c_void_p]),
     "snappy_amd_get_stream": (_c.c_void_p, [_c.c_void_p]),
+    "snappy_amd_device_bytes": (_c.c_size_t, [_c.c_void_p]),
+    "snappy_amd_trim": (_c.c_int, [_c.c_void_p]),
     "snappy_amd_num_units": (_c.c_size_t, [_c.c_size_t, _c.c_uint32, _c.c_int]),
     "snappy_amd_max_output": (_c.c_size_t, [_c.c_size_t, _c.c_uint32, _c.c_int]),
     "snappy_amd_compress_device": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_uint32, _c.c_int,
@@ -104,6 +106,8 @@ _SIGS = {
     # FILE* in, header value, FILE* out, FILE* sidecar (or NULL), bytes read (C stdio streams; the C host layer)
     "snappy_amd_host_compress_file": (_c.c_int, [_c.c_void_p, _c.c_uint64, _c.c_void_p, _c.c_void_p,
                                                  _c.POINTER(_c.c_uint64)]),
+    # FILE* in, sidecar entries (or NULL) and their count, FILE* out
+    "snappy_amd_host_decompress_file": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_void_p]),
     # reference Buffer cursor helpers (Buffer* is a struct of two pointers and a u32)
     "init_Buffer": (None, [_c.c_void_p, _c.c_uint]),
     "move_current": (None, [_c.c_void_p, _c.c_uint]),
@@ -270,6 +274,14 @@ class Codec:
     def set_stream(self, stream_ptr: int) -> None:
         _check(lib().snappy_amd_set_stream(self._h, ctypes.c_void_p(stream_ptr)), "set_stream")
 
+    def device_bytes(self) -> int:
+        """HBM bytes held as scratch by this context (grows to the largest call)."""
+        return lib().snappy_amd_device_bytes(self._h)
+
+    def trim(self) -> None:
+        """Free the context's scratch (the next call allocates it again)."""
+        _check(lib().snappy_amd_trim(self._h), "trim")
+
     def enable_timing(self, on: bool = True) -> None:
         _check(lib().snappy_amd_enable_timing(self._h, 1 if on else 0), "enable_timing")
 
@@ -360,6 +372,6 @@ class Codec:
         units_max = (1 << 20)
         offs = torch.empty(units_max + 1, dtype=torch.int64, device=comp.device)
         self._bind_stream()
-        n = self.index_ptr(comp.data_ptr(), comp.numel(), offs.data_ptr(), units_max)
+        n = self.index_ptr(comp.data_ptr(), comp.numel(), offs.data_ptr(), units_max + 1)
         units = (n + BLOCK - 1) // BLOCK
         return n, offs[: units + 1]

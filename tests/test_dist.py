@@ -170,12 +170,14 @@ def _bench(*args):
 
 @pytest.mark.gpu
 def test_bench_spawns_ranks_weak():
-    """bench.py --gpus 2 (no launcher): spawns two ranks (gloo rehearsal on one
-    GPU), prints one line with n_gpus 2, C2/C3 timed and verified."""
-    d = _bench("--gpus", "2", "--dist-backend", "gloo", "--bytes-per-gpu", str(64 << 20), "--steps", "2",
-               "--warmup", "1", "--no-host-e2e")
+    """bench.py --gpus 2 --weak (no launcher): spawns two ranks (gloo rehearsal
+    on one GPU), prints one line with n_gpus 2; the end-to-end loop (compress,
+    C1, C2, compaction, decode from the stream) and C3 are timed and verified."""
+    d = _bench("--gpus", "2", "--weak", "--dist-backend", "gloo", "--bytes-per-gpu", str(64 << 20), "--steps", "2",
+               "--warmup", "1", "--no-host-e2e", "--c3")
     assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["round_trip_ok"]
-    assert d["exchange"]["verified"] and d["exchange"]["c2_stream_allgather"]["ms"] > 0
+    assert d["exchange"]["verified"] and d["value_end_to_end"] > 0
+    assert d["exchange"]["c3_decoded_allgather"]["verified"]
     assert d["config"]["total_bytes"] == 2 * (64 << 20)
 
 
@@ -188,3 +190,35 @@ def test_bench_strong_pieces():
                "--no-host-e2e")
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["round_trip_ok"]
     assert d["config"]["pieces_per_gpu"] == 3 and d["exchange"]["verified"]
+    # the reassembled SINGLE stream: every byte once, in order
+    assert d["exchange"]["stream_bytes"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_memory_within_plan(world):
+    """Per-rank device memory of a scaled strong-scaling run (gloo ranks on one
+    GPU, text32k, pieces of 64 MiB) stays within dist.rank_plan for that size
+    -- the plan that DESIGN.md 6 extrapolates to 64 GiB at N = 1/2/4/8 (the
+    CPU test test_rank_plan_fits_hbm checks those fit 288 GB).  The measured
+    peak is the torch allocator's peak (shard, payload, decoded output, block
+    indexes, the C2 gather buffer and stream) plus the library's scratch."""
+    total = 384 << 20
+    d = _bench("--gpus", str(world), "--dist-backend", "gloo", "--total-bytes", str(total), "--piece-bytes",
+               str(64 << 20), "--steps", "1", "--warmup", "1", "--no-host-e2e")
+    m = d["memory"]
+    assert d["round_trip_ok"] and d["exchange"]["verified"]
+    assert 0 < m["rank_peak_bytes"] <= m["planned_peak_bytes_per_rank"], m
+    # the plan is a worst-case bound, not a vacuous one: text uses a good part of it
+    assert m["rank_peak_bytes"] >= 0.3 * m["planned_peak_bytes_per_rank"], m
+
+
+@pytest.mark.gpu
+def test_bench_rccl_world1():
+    """The RCCL (nccl backend) exchange code path on the one GPU a box has:
+    a 1-rank communicator runs C1 in every step and the end-to-end loop's C2
+    all-gather + compaction + decode from the reassembled stream."""
+    d = _bench("--dist-world1", "--dist-backend", "nccl", "--bytes-per-gpu", str(256 << 20), "--steps", "2",
+               "--warmup", "1", "--no-host-e2e", "--no-cpu-baseline", "--no-sub")
+    assert d["round_trip_ok"] and d["exchange"]["verified"] and d["exchange"]["backend"].startswith("nccl")
+    assert d["value_end_to_end"] > 0

@@ -495,3 +495,65 @@ def test_decompress_with_sidecar_index_xblock(codec, golden):
         idx = _index_file(n, [int(x) for x in offs.cpu().numpy()])
         out = snappy_amd.decompress_indexed(stream, idx)
         assert sha(out) == v["out_sha256"], v["name"]
+
+
+def test_index_misaligned_stream(codec):
+    """K5p on a stream at an odd device address (a foreign buffer at any
+    offset): the same index as at an aligned address, decoded bit-exact (the
+    chunk-parallel path, not the one-wave serial fallback of round 2)."""
+    import torch
+    a = datagen.make("T", 24 << 20, 61)
+    comp, offs = codec.compress_tensor(to_dev(a), layout=snappy_amd.SINGLE)
+    clen = comp.numel()
+    for shift in (1, 2, 3):
+        buf = torch.zeros(clen + 8, dtype=torch.uint8, device="cuda")
+        buf[shift:shift + clen] = comp
+        got = torch.empty_like(offs)
+        n = codec.index_ptr(buf.data_ptr() + shift, clen, got.data_ptr(), offs.numel())
+        assert n == a.size and torch.equal(got, offs), shift
+        back = torch.empty(a.size, dtype=torch.uint8, device="cuda")
+        codec.decompress_ptr(buf.data_ptr() + shift, got.data_ptr(), n, snappy_amd.BLOCK, snappy_amd.SINGLE,
+                             back.data_ptr())
+        assert torch.equal(back.cpu(), torch.from_numpy(a)), shift
+    # an index buffer one entry short is refused, not silently left without its last entry
+    with pytest.raises(snappy_amd.SnappyError) as ei:
+        codec.index_ptr(comp.data_ptr(), clen, got.data_ptr(), offs.numel() - 1)
+    assert ei.value.code == snappy_amd.ERR_CAPACITY
+
+
+def test_tampered_sidecar_index_refused(codec):
+    """a sidecar index whose middle entries point past the stream
+    or go backwards is refused with ERR_INDEX before any kernel reads it."""
+    a = datagen.make("T", 3 << 20, 62)
+    stream = oracle.compress(a.tobytes())
+    _, offs = codec.compress_tensor(to_dev(a), layout=snappy_amd.SINGLE)
+    ent = [int(v) for v in offs.cpu().numpy()]
+    assert snappy_amd.decompress_indexed(stream, _index_file(a.size, ent)) == a.tobytes()
+    for k, v in ((7, len(stream) + 4096), (20, ent[19] - 1), (1, 1 << 39)):
+        bad = list(ent)
+        bad[k] = v
+        with pytest.raises(snappy_amd.SnappyError) as ei:
+            snappy_amd.decompress_indexed(stream, _index_file(a.size, bad))
+        assert ei.value.code == snappy_amd.ERR_INDEX, k
+    with pytest.raises(snappy_amd.SnappyError) as ei:  # trailing bytes / short file
+        snappy_amd.decompress_indexed(stream, _index_file(a.size, ent) + b"\0")
+    assert ei.value.code == snappy_amd.ERR_INDEX
+    with pytest.raises(snappy_amd.SnappyError) as ei:
+        snappy_amd.read_index(b"SNPA")
+    assert ei.value.code == snappy_amd.ERR_INDEX
+
+
+def test_device_index_past_stream_end_fails_cleanly(codec):
+    """The HBM API trusts its index, but K4 never reads past the stream end the
+    last entry names: a middle entry beyond it is a per-unit error, and the
+    context decodes the next (good) stream normally."""
+    import torch
+    a = datagen.make("T", 4 << 20, 63)
+    x = to_dev(a)
+    comp, offs = codec.compress_tensor(x, layout=snappy_amd.SINGLE)
+    bad = offs.clone()
+    bad[3] = offs[-1] + (1 << 30)
+    with pytest.raises(snappy_amd.SnappyError):
+        codec.decompress_tensor(comp, bad, a.size, layout=snappy_amd.SINGLE)
+    back = codec.decompress_tensor(comp, offs, a.size, layout=snappy_amd.SINGLE)
+    assert torch.equal(back, x)

@@ -647,9 +647,21 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #ifdef SNAPPY_K1R_STATS
                 n_refresh++;
 #endif
-                // the deferred token stays pending (drained by the next round): count it
-                if (pend + dkn > 48) flush_tokens();
-                WINDOW_LS(p - 1);
+                // the deferred token stays pending (drained by the next round): count it.
+                // BIG: the window move waits vmcnt(0) for its staged LDS-DMA, and vmcnt
+                // counts stores too (in issue order): flush after the move, so that
+                // wait never covers this refresh's token stores
+#ifndef SNAPPY_K1R_FLUSH_FIRST
+                if constexpr (BIG) {
+                    const bool fl = pend + dkn > 48;
+                    WINDOW_LS(p - 1);
+                    if (fl) flush_tokens();
+                } else
+#endif
+                {
+                    if (pend + dkn > 48) flush_tokens();
+                    WINDOW_LS(p - 1);
+                }
                 LSTAMP(s6);
                 LSEG(5, s5, s6);
             };

@@ -1,0 +1,40 @@
+#!/bin/bash
+# One GPU-box session of checks (run from the repo root on the box):
+#   tools/gpu_session.sh <outdir> [tests] [bench] [n1_64g] [prof64g] [profile <workloads...>]
+# Every GPU step has its own time limit; a step that times out, aborts or
+# faults ends the session (exit codes 124/134/137/139 and signals), and a
+# failing pytest run (rc 1) is recorded but does not stop the benches.
+set -o pipefail
+export TMPDIR=/tmp
+out=${1:?outdir}; shift
+mkdir -p "$out"
+fatal() { case $1 in 0|1) return 1;; *) return 0;; esac; }
+for step in "$@"; do
+    echo "[$(date +%T)] $step"
+    case $step in
+    tests)
+        timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+            > "$out/gpu_tests.log" 2>&1
+        rc=$?; echo "tests rc=$rc"; tail -3 "$out/gpu_tests.log"
+        fatal $rc && exit $rc ;;
+    bench)
+        timeout -k 10 500 python -u bench.py --steps 20 --warmup 5 > "$out/bench.json" 2> "$out/bench.err"
+        rc=$?; echo "bench rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
+    n1_64g)  # the N = 1 point of configs[3]: 64 GiB of 32 KiB text streams on one GPU
+        timeout -k 10 600 python -u bench.py --total-bytes 68719476736 --steps 5 --warmup 1 \
+            --cpu-sample-bytes 268435456 > "$out/n1_64g.json" 2> "$out/n1_64g.err"
+        rc=$?; echo "n1_64g rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
+    prof64g)
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$out/n1_64g_trace" -o run --output-format csv -- \
+            python3 bench.py --total-bytes 68719476736 --steps 2 --warmup 1 --no-cpu-baseline --no-host-e2e \
+            > "$out/n1_64g_trace.log" 2>&1
+        rc=$?; echo "prof64g rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
+    ab:*)  # ab:<variant,variant,...>:<kind>:<chunk>:<layout> -> tools/variant_bench.py, 1 GiB
+        IFS=: read -r _ vs kind chunk layout <<< "$step"
+        timeout -k 10 400 python -u tools/variant_bench.py ${vs//,/ } --kind $kind --n 1073741824 --chunk $chunk \
+            --layout $layout --reps 3 --rounds 2 > "$out/ab_${kind}_${chunk}.log" 2>&1
+        rc=$?; echo "ab rc=$rc"; tail -6 "$out/ab_${kind}_${chunk}.log"; [ $rc -ne 0 ] && exit $rc ;;
+    *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
+echo "[$(date +%T)] done"

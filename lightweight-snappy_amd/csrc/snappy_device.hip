@@ -12,6 +12,7 @@
 #include <mutex>
 #include <sys/stat.h>
 #include <thread>
+#include <time.h>
 #include <unistd.h>
 #include <vector>
 
@@ -513,6 +514,20 @@ size_t read_full(FILE *f, uint8_t *b, size_t cap)
     return n;
 }
 
+// SNAPPY_AMD_IO_TRACE=1: phase times of the FILE* pipelines on stderr
+double io_now()
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+bool io_trace()
+{
+    static int on = -1;
+    if (on < 0) on = getenv("SNAPPY_AMD_IO_TRACE") != nullptr;
+    return on > 0;
+}
+
 // Threads copying file chunks between the page cache and pinned staging
 // (SNAPPY_AMD_IO_THREADS, default 8): one stdio thread moves a few GB/s, the
 // GPU path tens.
@@ -682,7 +697,10 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
     }
     HIP_OK(hipSetDevice(dev));
     uint64_t total_in = 0;
+    const double t0 = io_now();
+    double t_rd = 0, t_dr = 0;
     size_t n = in.read(g_slots[0].h_in, kStreamChunk);
+    t_rd += io_now() - t0;
     if (in.error()) return SNAPPY_AMD_ERR_IO;
     for (uint32_t k = 0; n > 0; k++) {
         StreamSlot &s = g_slots[k & 1];
@@ -697,8 +715,12 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
         s.busy = true;
         // chunk k-1 out while chunk k runs, then chunk k+1 in (its slot is free
         // once chunk k-1 drained)
+        const double td = io_now();
         if ((rc = slot_drain(o, out, fidx, &base))) return rc;
+        const double tr = io_now();
         n = in.read(o.h_in, kStreamChunk);
+        t_rd += io_now() - tr;
+        t_dr += tr - td;
         if (in.error()) return SNAPPY_AMD_ERR_IO;
     }
     // the slots drain in chunk order: the one holding the last chunk goes last
@@ -706,6 +728,11 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
     if ((rc = slot_drain(g_slots[last ^ 1], out, fidx, &base))) return rc;
     if ((rc = slot_drain(g_slots[last], out, fidx, &base))) return rc;
     if (!in.finish() || !out.finish()) return SNAPPY_AMD_ERR_IO;
+    if (io_trace())
+        fprintf(stderr, "[snappy_amd io] compress %llu -> %llu B: %.3f s (reads %.3f, drain+writes %.3f), %d threads, "
+                        "positional in %d out %d\n",
+                (unsigned long long)total_in, (unsigned long long)base, io_now() - t0, t_rd, t_dr, io_threads(),
+                (int)in.pos_io, (int)out.pos_io);
     if (fidx) {
         // the stream's preamble says header_value; an index is only valid for a
         // stream whose preamble is the length actually compressed
@@ -815,18 +842,23 @@ int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count
     if ((rc = grow(reinterpret_cast<void **>(&c->d_a), &c->d_a_cap, n + 16))) return rc;
     // (1) file -> pinned chunk k % 3 (host threads) -> HBM (copy engine), the
     // next chunk read while this one is copied
+    const double t0 = io_now();
+    double t_rd = 0;
     uint64_t N = 0;
     const uint64_t nch = (n + kStreamChunk - 1) / kStreamChunk;
     for (uint64_t k = 0; k < nch; k++) {
         const int s = (int)(k % 3);
         if (k >= 3) HIP_OK(hipEventSynchronize(g_dec.ev[s]));
         const size_t m = (size_t)std::min<uint64_t>(kStreamChunk, n - k * kStreamChunk);
+        const double tr = io_now();
         if (in.read(g_dec.h[s], m) != m) return SNAPPY_AMD_ERR_IO;
+        t_rd += io_now() - tr;
         if (k == 0 && snappy_varint_decode(g_dec.h[0], m, &N) == 0) return SNAPPY_AMD_ERR_HEADER;
         HIP_OK(hipMemcpyAsync(c->d_a + k * kStreamChunk, g_dec.h[s], m, hipMemcpyHostToDevice, c->stream));
         HIP_OK(hipEventRecord(g_dec.ev[s], c->stream));
     }
     if (!in.finish()) return SNAPPY_AMD_ERR_IO;
+    const double t1 = io_now();
     // (2) block index (sidecar, checked, or the GPU index pass) and decode
     const uint64_t units = (N + SNAPPY_AMD_BLOCK - 1) / SNAPPY_AMD_BLOCK;
     if ((rc = grow(reinterpret_cast<void **>(&c->d_b), &c->d_b_cap, N + 16))) return rc;
@@ -847,6 +879,8 @@ int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count
         return rc;
     // (3) HBM -> pinned chunk (copy engine) -> file (host threads), the next
     // chunk copied down while this one is written
+    const double t2 = io_now();
+    double t_wr = 0;
     if (!out.open(fout, true)) return SNAPPY_AMD_ERR_IO;
     const uint64_t och = (N + kStreamChunk - 1) / kStreamChunk;
     auto down = [&](uint64_t k) -> int {
@@ -860,9 +894,17 @@ int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count
         if (k + 1 < och && (rc = down(k + 1))) return rc;
         HIP_OK(hipEventSynchronize(g_dec.ev[k % 3]));
         const size_t m = (size_t)std::min<uint64_t>(kStreamChunk, N - k * kStreamChunk);
+        const double tw = io_now();
         if (!out.write(g_dec.h[k % 3], m)) return SNAPPY_AMD_ERR_IO;
+        t_wr += io_now() - tw;
     }
-    return out.finish() ? SNAPPY_AMD_OK : SNAPPY_AMD_ERR_IO;
+    const bool fin_ok = out.finish();
+    if (io_trace())
+        fprintf(stderr, "[snappy_amd io] decompress %llu -> %llu B: in %.3f s (reads %.3f), index+decode %.3f s, "
+                        "out %.3f s (writes %.3f), %d threads, positional out %d\n",
+                (unsigned long long)n, (unsigned long long)N, t1 - t0, t_rd, t2 - t1, io_now() - t2, t_wr,
+                io_threads(), (int)out.pos_io);
+    return fin_ok ? SNAPPY_AMD_OK : SNAPPY_AMD_ERR_IO;
 }
 
 }  // extern "C"

@@ -673,7 +673,13 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             // the round's table entries: read once per round, at its end, after every
             // insert of the round (one definition, so no register copy waits for it)
             ent = TBL_READ3(adr);
-            for (;;) {
+#ifdef SNAPPY_K1R_OLD_EXIT
+            for (;;)
+#else
+            bool go = true;
+            do
+#endif
+            {
                 LSTAMP(s0);
                 drain_token();  // the previous round's match: one writelane pair per round
                 // probe k = lane - lane0 for k <= kcap: step 1 before it ((skip + k - 1) >> 5 == 1),
@@ -770,6 +776,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #ifdef SNAPPY_K1R_STATS
                 n_round++;
 #endif
+#ifdef SNAPPY_K1R_OLD_EXIT
                 // is_block_end at skip < 64; steps > 1 continue in W-probe rounds
                 if (__builtin_expect(!(skip <= 64 - SNAPPY_K1R_LSMIN && p <= L - 16), 0)) break;
                 lane0 = p - q0;
@@ -777,8 +784,26 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     refresh();
                     lane0 = 1;
                 }
+#else
+                lane0 = p - q0;
+                // the three rare ends of a run of rounds -- a step past 1, is_block_end,
+                // the window refresh -- in one sign test (every term is < 2^31); the
+                // loop's only exit is its latch (no flow masks on the common path)
+                if (__builtin_expect((int32_t)((64 - SNAPPY_K1R_LSMIN - skip) | (L - 16 - p) |
+                                               (62 - SNAPPY_K1R_RMIN - lane0)) < 0, 0)) {
+                    // is_block_end at skip < 64; steps > 1 continue in W-probe rounds
+                    go = skip <= 64 - SNAPPY_K1R_LSMIN && p <= L - 16;
+                    if (go) {
+                        refresh();
+                        lane0 = 1;
+                    }
+                }
+#endif
                 ent = TBL_READ3(adr);
             }
+#ifndef SNAPPY_K1R_OLD_EXIT
+            while (go);
+#endif
             drain_token();
 #ifdef SNAPPY_K1R_STATS
             n_round--;

@@ -34,6 +34,16 @@ for step in "$@"; do
         timeout -k 10 400 python -u tools/variant_bench.py ${vs//,/ } --kind $kind --n 1073741824 --chunk $chunk \
             --layout $layout --reps 3 --rounds 2 > "$out/ab_${kind}_${chunk}.log" 2>&1
         rc=$?; echo "ab rc=$rc"; tail -6 "$out/ab_${kind}_${chunk}.log"; [ $rc -ne 0 ] && exit $rc ;;
+    counters)
+        timeout -k 10 120 rocprofv3 --list-avail > "$out/counters.txt" 2>&1
+        rc=$?; echo "counters rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
+    occ:*)  # occ:<kind>:<chunk>:<dynlds,...> -> K1r statistics build at reduced occupancy
+        IFS=: read -r _ kind chunk dyns <<< "$step"
+        for d in ${dyns//,/ }; do
+            SNAPPY_K1R_DYNLDS=$d timeout -k 10 200 python -u tools/k1r_stats.py $kind 268435456 $chunk \
+                > "$out/occ_${kind}_${chunk}_$d.log" 2>&1
+            rc=$?; echo "occ $d rc=$rc"; cat "$out/occ_${kind}_${chunk}_$d.log"; [ $rc -ne 0 ] && exit $rc
+        done ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -40,6 +40,7 @@ constexpr uint32_t kTable = 4096;
 constexpr uint32_t kMul = 0x1e35a7bdu;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -350,10 +351,10 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     // the next record's), a ds_write_b16 + ds_write_b8_d16_hi store one; the
     // highest lane wins a record shared within one instruction pair
     // (tools/micro/lds_packed3.hip).  12 units/CU (with the VGPR limit).
+#ifdef SNAPPY_K1R_PACKED3
     __shared__ __attribute__((aligned(16))) uint8_t tbl_[3 * kTable + 8];
     constexpr uint32_t kDummy = 3 * kTable + 4;  // a record nobody reads: the target of non-inserting lanes
     auto *const tbl = (__attribute__((address_space(3))) uint8_t *)tbl_;
-#define TAG_OF(v) (((v) * kTagMul) >> 24)
 #define TBL_READ3(adr) (*(__attribute__((address_space(3))) u32u *)(tbl + (adr)))
 #define TBL_WRITE3(adr, word)                                                                       \
     do {                                                                                           \
@@ -361,8 +362,57 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         *(__attribute__((address_space(3))) u16u *)(tbl + _a) = (uint16_t)_w;                       \
         tbl[_a + 2] = (uint8_t)(_w >> 16);                                                         \
     } while (0)
+#define TBL_ADR(h) (3 * (h))
+#define TBL_READ_ENT(adr) do { ent = TBL_READ3(adr); ent_t = ent >> 16; } while (0)
 #define TBL_READ(h) TBL_READ3(3 * (h))
 #define TBL_WRITE(s, word) TBL_WRITE3(3 * (s), word)
+#else
+    // The same 12 KiB as two aligned arrays: u16 positions at byte 2 * slot and
+    // u8 tags at kTagBase + slot, so no table access is unaligned (the packed
+    // 3-byte records measured SQ_LDS_UNALIGNED_STALL 8.5e9 per 1 GiB launch:
+    // the LDS spent most of its active cycles stalled on them).  A record's
+    // address is that of its position (`adr` = 2 * slot); its tag sits at
+    // adr / 2 + kTagBase.  Reads: ds_read_u16 + ds_read_u8; writes:
+    // ds_write_b16 + ds_write_b8_d16_hi, each highest-lane-wins on its own
+    // address, so a record shared within one write pair is the same lane's.
+    // slot kTable: a record nobody reads, the target of non-inserting lanes (one
+    // per lane instead -- no same-address writes -- measured 2.6 % slower: 16.86
+    // against 16.42 ms per GiB of 32 KiB text streams)
+    constexpr uint32_t kSlots = kTable + 1;
+    constexpr uint32_t kTagBase = 2 * kSlots + 6;
+    __shared__ __attribute__((aligned(16))) uint8_t tbl_[kTagBase + kSlots + 7];
+    constexpr uint32_t kDummy = 2 * kTable;
+    auto *const tbl = (__attribute__((address_space(3))) uint8_t *)tbl_;
+    // (the two halves are loaded into one register as a 2 x u16 vector, so the
+    // backend can use ds_read_u16_d16 + ds_read_u8_d16_hi: no VALU joins them,
+    // so no wait is forced where the read is issued)
+#define TBL_READ3(adr)                                                                              \
+    ({                                                                                             \
+        const uint32_t _a = (adr);                                                                 \
+        u16x2 _v;                                                                                  \
+        _v.x = *(__attribute__((address_space(3))) uint16_t *)(tbl + _a);                          \
+        _v.y = (uint16_t)tbl[(_a >> 1) + kTagBase];                                                \
+        __builtin_bit_cast(uint32_t, _v);                                                          \
+    })
+#define TBL_WRITE3(adr, word)                                                                       \
+    do {                                                                                           \
+        const uint32_t _a = (adr), _w = (word);                                                    \
+        *(__attribute__((address_space(3))) uint16_t *)(tbl + _a) = (uint16_t)_w;                   \
+        tbl[(_a >> 1) + kTagBase] = (uint8_t)(_w >> 16);                                           \
+    } while (0)
+#define TBL_ADR(h) (2 * (h))
+// lane-space rounds: position and tag as two registers (nothing joins the two
+// loads, so their wait sits at the first use, not where they are issued)
+#define TBL_READ_ENT(adr)                                                                           \
+    do {                                                                                           \
+        const uint32_t _a = (adr);                                                                 \
+        ent = *(__attribute__((address_space(3))) uint16_t *)(tbl + _a);                           \
+        ent_t = tbl[(_a >> 1) + kTagBase];                                                         \
+    } while (0)
+#define TBL_READ(h) TBL_READ3(2 * (h))
+#define TBL_WRITE(s, word) TBL_WRITE3(2 * (s), word)
+#endif
+#define TAG_OF(v) (((v) * kTagMul) >> 24)
 // Lanes communicate through the table: a read must see every earlier write of
 // the wave, including other lanes' (LDS executes a wave's accesses in order).
 // C++ sees no such dependence, so every write group is followed by a compiler
@@ -529,6 +579,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     // rotated: dword q0/4 + i sits at lane (dr + i) % 64 (ds_bpermute wraps addr[7:2])
     uint32_t q0 = 0, d0 = 0, dr = 0, dv = 0, bv = 0, hv = 0;
     uint32_t pdl1 = 0, pdc = 0, ent = 0;      // lane-space data: predecessor lane + 1, its position, entry
+    uint32_t ent_t = 0;                       // the entry's tag (bits 0..7; split table: its own load)
     uint32_t adr = 0, word = 0;               // the lane's table record address and its insert word
     uint32_t pdnz = 0;
     uint64_t m_win = 0, m_win17 = 0;
@@ -564,7 +615,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         const int32_t _w16 = (int32_t)(L - 16 - q0), _w17 = (int32_t)(L - 17 - q0);              \
         m_win = __ballot((int32_t)lane <= _w16 && lane <= 62);                                     \
         m_win17 = __ballot((int32_t)lane <= _w17 && lane <= 62);                                   \
-        adr = 3 * (hv & 0xFFFF);                                                                   \
+        adr = TBL_ADR(hv & 0xFFFF);                                                                \
         word = (q0 + lane) | (hv & 0xFF0000u);                                                     \
         lsw = true; /* the caller reads ent */                                                     \
     } while (0)
@@ -672,14 +723,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             }
             // the round's table entries: read once per round, at its end, after every
             // insert of the round (one definition, so no register copy waits for it)
-            ent = TBL_READ3(adr);
-#ifdef SNAPPY_K1R_OLD_EXIT
-            for (;;)
-#else
-            bool go = true;
-            do
-#endif
-            {
+            TBL_READ_ENT(adr);
+            for (;;) {
                 LSTAMP(s0);
                 drain_token();  // the previous round's match: one writelane pair per round
                 // probe k = lane - lane0 for k <= kcap: step 1 before it ((skip + k - 1) >> 5 == 1),
@@ -696,7 +741,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 // lane l > lane0 takes the in-round candidate when its nearest same-hash lane is >= lane0 - 1;
                 // the hit test selects per lane (VALU) so one ballot carries it to SALU
                 const bool inr = (int32_t)pdl1 >= (int32_t)lane0;
-                const uint32_t hitnz = inr ? pdnz : ((ent ^ word) & 0xFF0000u);
+                const uint32_t hitnz = inr ? pdnz : ((ent_t ^ (word >> 16)) & 0xFFu);
                 const uint64_t hm = __ballot(hitnz == 0) & valid;
                 const uint32_t candv = inr ? pdc : ent;
                 const uint32_t f = (uint32_t)__builtin_ctzll(hm);
@@ -776,7 +821,6 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #ifdef SNAPPY_K1R_STATS
                 n_round++;
 #endif
-#ifdef SNAPPY_K1R_OLD_EXIT
                 // is_block_end at skip < 64; steps > 1 continue in W-probe rounds
                 if (__builtin_expect(!(skip <= 64 - SNAPPY_K1R_LSMIN && p <= L - 16), 0)) break;
                 lane0 = p - q0;
@@ -784,26 +828,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     refresh();
                     lane0 = 1;
                 }
-#else
-                lane0 = p - q0;
-                // the three rare ends of a run of rounds -- a step past 1, is_block_end,
-                // the window refresh -- in one sign test (every term is < 2^31); the
-                // loop's only exit is its latch (no flow masks on the common path)
-                if (__builtin_expect((int32_t)((64 - SNAPPY_K1R_LSMIN - skip) | (L - 16 - p) |
-                                               (62 - SNAPPY_K1R_RMIN - lane0)) < 0, 0)) {
-                    // is_block_end at skip < 64; steps > 1 continue in W-probe rounds
-                    go = skip <= 64 - SNAPPY_K1R_LSMIN && p <= L - 16;
-                    if (go) {
-                        refresh();
-                        lane0 = 1;
-                    }
-                }
-#endif
-                ent = TBL_READ3(adr);
+                TBL_READ_ENT(adr);
             }
-#ifndef SNAPPY_K1R_OLD_EXIT
-            while (go);
-#endif
             drain_token();
 #ifdef SNAPPY_K1R_STATS
             n_round--;
@@ -880,6 +906,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #undef TBL_WRITE
 #undef TBL_READ3
 #undef TBL_WRITE3
+#undef TBL_ADR
+#undef TBL_READ_ENT
 #undef TAG_EQ
 #undef LDS_ORDER
 #undef CAND_LANES

@@ -34,6 +34,12 @@ for step in "$@"; do
         timeout -k 10 400 python -u tools/variant_bench.py ${vs//,/ } --kind $kind --n 1073741824 --chunk $chunk \
             --layout $layout --reps 3 --rounds 2 > "$out/ab_${kind}_${chunk}.log" 2>&1
         rc=$?; echo "ab rc=$rc"; tail -6 "$out/ab_${kind}_${chunk}.log"; [ $rc -ne 0 ] && exit $rc ;;
+    pmc:*)  # pmc:<tag>:<workload>:<COUNTER,COUNTER,...> -> one rocprofv3 counter pass over a 1-step bench
+        IFS=: read -r _ tag wl ctrs <<< "$step"
+        timeout -s KILL 240 rocprofv3 --pmc ${ctrs//,/ } --kernel-trace -d "$out/pmc_$tag" -o run \
+            --output-format csv -- python3 bench.py --workload $wl --steps 1 --warmup 1 --no-cpu-baseline \
+            --no-host-e2e --no-sub > "$out/pmc_$tag.log" 2>&1
+        rc=$?; echo "pmc $tag rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
     counters)
         timeout -k 10 120 rocprofv3 --list-avail > "$out/counters.txt" 2>&1
         rc=$?; echo "counters rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;

@@ -1056,7 +1056,7 @@ __device__ __forceinline__ void put_element_lds(__attribute__((address_space(3))
                                                 uint32_t hl, uint32_t len, uint32_t off, bool wide_ok, bool live,
                                                 uint32_t lane, const uint32_t *lw, uint32_t sh)
 {
-    const uint32_t dum = kK2Stage + 4 * lane;
+    const uint32_t dum = kK2Stage + 4 + 4 * lane;  // past the stage and its 3 alignment bytes
 #define K2_ST8(cond, adr, v) stage[(cond) ? (adr) : dum] = (uint8_t)(v)
     // literal header (write_literal :95-120)
     const uint32_t lm1 = litn - 1;
@@ -1183,7 +1183,7 @@ __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(cons
                                                     const uint32_t *__restrict__ seg_off, uint32_t segs,
                                                     const uint64_t *__restrict__ offsets, uint8_t *__restrict__ out)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t stage_[kK2Stage + 4 * 64 + 16];  // + per-lane dummy slots
+    __shared__ __attribute__((aligned(16))) uint8_t stage_[kK2Stage + 4 + 4 * 64 + 16];  // + alignment, per-lane dummies
     auto *const stage = (__attribute__((address_space(3))) uint8_t *)stage_;
     const uint32_t lane = threadIdx.x;
     const uint32_t u = blockIdx.x;
@@ -1250,6 +1250,9 @@ __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(cons
     uint32_t total;
     uint32_t rel = wave_excl_scan(lsum, lane, &total);
     const bool staged = total <= kK2Stage;
+    // the stage is laid out at the destination's alignment (stage byte sb + x is
+    // output byte dst + o + x), so the copy-out below reads aligned LDS dwords
+    const uint32_t sb = staged ? (uint32_t)(reinterpret_cast<uintptr_t>(dst + o) & 3) : 0u;
     uint64_t longs[kK2Per];
     uint32_t d0v[kK2Per];
     // every short literal's source dwords in one round trip: lanes with none read
@@ -1270,11 +1273,11 @@ __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(cons
 #pragma unroll
     for (uint32_t i = 0; i < kK2Per; i++) {
         const bool wide_ok = wide[i];
-        if (staged) put_element_lds(stage, rel, src, pe[i], litn[i], hl[i], len[i], off[i], wide_ok, live[i], lane,
+        if (staged) put_element_lds(stage, rel + sb, src, pe[i], litn[i], hl[i], len[i], off[i], wide_ok, live[i], lane,
                                     lw[i], lsh[i]);
         else if (live[i]) put_element(dst + o + rel, src, pe[i], litn[i], hl[i], len[i], off[i], wide_ok);
         longs[i] = __ballot(live[i] && litn[i] > 16);
-        d0v[i] = rel + hl[i];
+        d0v[i] = rel + sb + hl[i];
         rel += sz[i];
     }
 #pragma unroll
@@ -1284,17 +1287,18 @@ __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(cons
     }
     if (staged) {
         __builtin_amdgcn_wave_barrier();
-        // stage[0, total) -> dst + o: byte head to a dword boundary, dwords, byte tail
+        // stage[sb, sb + total) -> dst + o: byte head to a dword boundary, aligned
+        // dwords (aligned in LDS too: sb + head is a multiple of 4), byte tail
         uint8_t *g = dst + o;
-        uint32_t head = (uint32_t)((4 - (reinterpret_cast<uintptr_t>(g) & 3)) & 3);
+        uint32_t head = (4 - sb) & 3;
         if (head > total) head = total;
-        if (lane < head) g[lane] = stage[lane];
+        if (lane < head) g[lane] = stage[sb + lane];
         const uint32_t nw = (total - head) >> 2;
         uint32_t *gw = reinterpret_cast<uint32_t *>(g + head);
-        for (uint32_t k = lane; k < nw; k += 64)
-            gw[k] = *(const __attribute__((address_space(3))) u32u *)(stage + head + 4 * k);
+        const auto *sw = reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(stage + sb + head);
+        for (uint32_t k = lane; k < nw; k += 64) gw[k] = sw[k];
         const uint32_t tail0 = head + 4 * nw;
-        if (lane < total - tail0) g[tail0 + lane] = stage[tail0 + lane];
+        if (lane < total - tail0) g[tail0 + lane] = stage[sb + tail0 + lane];
     }
     __builtin_amdgcn_wave_barrier();  // the stage is reused by the next pass
     o += total;

@@ -413,6 +413,14 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #define TBL_WRITE(s, word) TBL_WRITE3(2 * (s), word)
 #endif
 #define TAG_OF(v) (((v) * kTagMul) >> 24)
+// an insert group: the lanes where cond holds write their record; the others
+// either write the dummy record (one instruction stream, no exec change) or,
+// SNAPPY_K1R_MASKED_WRITES, are masked off
+#ifdef SNAPPY_K1R_MASKED_WRITES
+#define TBL_INSERT(cond) do { if (cond) TBL_WRITE3(adr, word); } while (0)
+#else
+#define TBL_INSERT(cond) TBL_WRITE3((cond) ? adr : kDummy, word)
+#endif
 // Lanes communicate through the table: a read must see every earlier write of
 // the wave, including other lanes' (LDS executes a wave's accesses in order).
 // C++ sees no such dependence, so every write group is followed by a compiler
@@ -762,7 +770,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     // first probe (its p - 1 is inserted only if it misses); other lanes
                     // write the dummy record
                     const uint32_t lo0 = f > lane0 ? lane0 - 1 : lane0;
-                    TBL_WRITE3(lane - lo0 <= f - lo0 ? adr : kDummy, word);
+                    TBL_INSERT(lane - lo0 <= f - lo0);
                     LDS_ORDER();
                     LSTAMP(s2);
                     LSEG(1, s1, s2);
@@ -795,7 +803,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     } else {  // tag collision: a miss (append_literal :283-287 steps by skip >> 5)
                         dkn = 0;
                         if (f == lane0) {  // its p - 1, then p again (the later write wins)
-                            TBL_WRITE3(lane - (lane0 - 1) <= 1 ? adr : kDummy, word);
+                            TBL_INSERT(lane - (lane0 - 1) <= 1);
                             LDS_ORDER();
                         }
                         np = pf + ((skip + f - lane0) >> 5);
@@ -806,7 +814,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     dka = dkb = dkn = 0;
                     const uint32_t nk = (uint32_t)__builtin_popcountll(valid);  // lanes lane0 .. lane0 + nk - 1
                     // update_hash_table :303-307: p_k - 1 and p_k of every miss, lane order
-                    TBL_WRITE3(lane - (lane0 - 1) <= nk ? adr : kDummy, word);
+                    TBL_INSERT(lane - (lane0 - 1) <= nk);
                     LDS_ORDER();
                     np = q0 + lane0 + nk - 1 + ((skip + nk - 1) >> 5);  // the last probe steps by 2 at skip 64
                     skip += nk;
@@ -828,7 +836,12 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     refresh();
                     lane0 = 1;
                 }
+#ifdef SNAPPY_K1R_MASKED_READS
+                // only the probe lanes need their entries (fewer bank conflicts)
+                if (lane - lane0 < DMAX) TBL_READ_ENT(adr);
+#else
                 TBL_READ_ENT(adr);
+#endif
             }
             drain_token();
 #ifdef SNAPPY_K1R_STATS
@@ -908,6 +921,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #undef TBL_WRITE3
 #undef TBL_ADR
 #undef TBL_READ_ENT
+#undef TBL_INSERT
 #undef TAG_EQ
 #undef LDS_ORDER
 #undef CAND_LANES

@@ -71,25 +71,6 @@ static int grow(void **ptr, size_t *cap, size_t need)
     return SNAPPY_AMD_OK;
 }
 
-// K4 output ring: the whole unit when it fits 4 KiB, else a 4 KiB ring (the
-// wave-slot limit, 28 units per CU at 85 SGPRs, binds before LDS does; copies
-// reaching further back read HBM).  SNAPPY_AMD_K4_RING overrides (power of
-// two >= 4 KiB).
-static uint32_t k4_ring_bytes(uint32_t unit)
-{
-    static uint32_t cap = 0;
-    if (!cap) {
-        cap = 4096;
-        if (const char *e = getenv("SNAPPY_AMD_K4_RING")) {
-            const unsigned long v = strtoul(e, nullptr, 10);
-            if (v >= 4096 && v <= 65536 && (v & (v - 1)) == 0) cap = (uint32_t)v;
-        }
-    }
-    uint32_t r = 1024;
-    while (r < unit && r < cap) r <<= 1;
-    return r;
-}
-
 extern "C" {
 
 int snappy_amd_create(int device, snappy_amd_ctx **out)
@@ -110,11 +91,6 @@ int snappy_amd_create(int device, snappy_amd_ctx **out)
         return SNAPPY_AMD_ERR_DEVICE;
     }
     for (int i = 0; i < 5; i++) (void)hipEventCreate(&c->ev[i]);
-    // K4's ring may be raised to 64 KiB (SNAPPY_AMD_K4_RING)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k4_decompress_units),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k4_decompress_back),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     *out = c;
     return SNAPPY_AMD_OK;
 }
@@ -312,19 +288,17 @@ static int decompress_launch(snappy_amd_ctx *c, const void *d_comp, const uint64
     const uint32_t allow_back = layout == SNAPPY_AMD_SINGLE ? 1u : 0u;
     if (c->timing) (void)hipEventRecord(c->ev[3], c->stream);
     if (allow_back) HIP_OK(hipMemsetAsync(c->status + units, 0, 2 * sizeof(int32_t), c->stream));
-    const uint32_t ring = k4_ring_bytes(unit);
     const uint32_t hm = hdr_mode_of(layout, flags);
-    // dynamic LDS: the ring + per-unit scalars + the compressed-input window
     // the kernel reads aligned dwords: pass the stream as an aligned base + bias
     const uint32_t bias = (uint32_t)(reinterpret_cast<uintptr_t>(d_comp) & 3);
     const uint8_t *comp = static_cast<const uint8_t *>(d_comp) - bias;
-    hipLaunchKernelGGL(k4_decompress_units, dim3((uint32_t)units), dim3(64), ring + SNAPPY_K4_LDS_EXTRA, c->stream, comp, d_offsets,
-                       (uint64_t)n, unit, hm, header_value, ring, allow_back, bias, static_cast<uint8_t *>(d_out),
+    hipLaunchKernelGGL(k4_decompress_units, dim3((uint32_t)units), dim3(64), 0, c->stream, comp, d_offsets,
+                       (uint64_t)n, unit, hm, header_value, allow_back, bias, static_cast<uint8_t *>(d_out),
                        c->status);
     HIP_OK(hipGetLastError());
     if (allow_back) {
-        hipLaunchKernelGGL(k4_decompress_back, dim3((uint32_t)units), dim3(64), ring + SNAPPY_K4_LDS_EXTRA, c->stream, comp,
-                           d_offsets, (uint64_t)n, unit, hm, header_value, ring, bias, static_cast<uint8_t *>(d_out),
+        hipLaunchKernelGGL(k4_decompress_back, dim3((uint32_t)units), dim3(64), 0, c->stream, comp,
+                           d_offsets, (uint64_t)n, unit, hm, header_value, bias, static_cast<uint8_t *>(d_out),
                            c->status);
         HIP_OK(hipGetLastError());
     }

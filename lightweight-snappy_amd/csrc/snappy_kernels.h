@@ -57,16 +57,13 @@ __global__ void k3_scan(const uint32_t *__restrict__ sizes, uint64_t count, uint
 // status SNAPPY_ST_DEFER, for pass 2, and set status[units + 1])
 __global__ void k4_decompress_units(const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets,
                                     uint64_t n, uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
-                                    uint32_t ring, uint32_t allow_back, uint32_t bias, uint8_t *__restrict__ out,
+                                    uint32_t allow_back, uint32_t bias, uint8_t *__restrict__ out,
                                     int32_t *__restrict__ status);
-// K4 dynamic LDS = the output ring + this: 16 bytes of per-unit scalars and
-// the 784-byte compressed-input window (3 x 256 + a 16-byte mirror)
-#define SNAPPY_K4_LDS_EXTRA 800u
 // K4 pass 2: the DEFER units, in ticket order (status[units] = ticket counter,
 // status[units + 1] = pass 1's defer flag; both 0 before pass 1)
 __global__ void k4_decompress_back(const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets,
                                    uint64_t n, uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
-                                   uint32_t ring, uint32_t bias, uint8_t *__restrict__ out,
+                                   uint32_t bias, uint8_t *__restrict__ out,
                                    int32_t *__restrict__ status);
 #ifndef SNAPPY_K5_CHUNK
 #define SNAPPY_K5_CHUNK 16384

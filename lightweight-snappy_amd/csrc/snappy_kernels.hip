@@ -270,7 +270,8 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
 }
 
 #ifndef SNAPPY_K1R_DMAX
-#define SNAPPY_K1R_DMAX 16  // lane-space rounds: same-hash distances resolved per window
+#define SNAPPY_K1R_DMAX 10  // lane-space rounds: same-hash distances resolved per window
+                            // (8/10/12/14/16 measured; profiles/r03h_ab_k1r_dmax_rmin_*)
 #endif
 #ifndef SNAPPY_K1R_LSMIN
 #define SNAPPY_K1R_LSMIN 4  // lane-space rounds while at least this many step-1 probes remain
@@ -414,13 +415,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #endif
 #define TAG_OF(v) (((v) * kTagMul) >> 24)
 // an insert group: the lanes where cond holds write their record; the others
-// either write the dummy record (one instruction stream, no exec change) or,
-// SNAPPY_K1R_MASKED_WRITES, are masked off
-#ifdef SNAPPY_K1R_MASKED_WRITES
-#define TBL_INSERT(cond) do { if (cond) TBL_WRITE3(adr, word); } while (0)
-#else
+// write the dummy record (one instruction stream, no exec change: masking
+// them off measured 3 % slower, profiles/r03j_ab_k1r_masked_*)
 #define TBL_INSERT(cond) TBL_WRITE3((cond) ? adr : kDummy, word)
-#endif
 // Lanes communicate through the table: a read must see every earlier write of
 // the wave, including other lanes' (LDS executes a wave's accesses in order).
 // C++ sees no such dependence, so every write group is followed by a compiler
@@ -836,12 +833,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     refresh();
                     lane0 = 1;
                 }
-#ifdef SNAPPY_K1R_MASKED_READS
-                // only the probe lanes need their entries (fewer bank conflicts)
-                if (lane - lane0 < DMAX) TBL_READ_ENT(adr);
-#else
-                TBL_READ_ENT(adr);
-#endif
+                TBL_READ_ENT(adr);  // every lane (reading only the probe lanes' measured 2.6 % slower)
             }
             drain_token();
 #ifdef SNAPPY_K1R_STATS
@@ -1508,6 +1500,8 @@ __device__ __noinline__ int32_t k4_wait(const int32_t *status, uint64_t g_lo, ui
 #ifdef SNAPPY_K4_STATS
 #if SNAPPY_TU_DECODE
 __device__ uint64_t g_k4_stats[32768 * 8];
+#else
+static __device__ uint64_t g_k4_stats[8];  // (k4_body is parsed, never instantiated, here)
 #endif
 #define K4STAMP(var)                                                                        \
     do {                                                                                    \
@@ -1519,17 +1513,25 @@ __device__ uint64_t g_k4_stats[32768 * 8];
 #define K4STAMP(var) do { } while (0)
 #endif
 
+// K4's LDS (static, so every base folds into the ds offset field): the
+// output ring, the batch's element-start bitmap, two scalars, the window
+constexpr uint32_t kK4Ring = 4096;    // output ring; copies reaching further back read HBM
+constexpr uint32_t kK4MapBits = 1024; // a batch's output span (bit j = an element starts at op + j)
+constexpr uint32_t kK4Lds = kK4Ring + kK4MapBits / 8 + 16 + 784;  // 5,024 B: 32 waves per CU fit 160 KiB
+
 template <bool BACK>
 __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets,
                                         uint64_t n, uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
-                                        uint32_t ring, uint32_t allow_back, uint32_t bias, uint8_t *__restrict__ out,
+                                        uint32_t allow_back, uint32_t bias, uint8_t *__restrict__ out,
                                         int32_t *__restrict__ status, uint32_t u)
 {
     // copy source positions: relative to the unit start, negative = an earlier unit (pass 2 only)
     using SrcT = typename std::conditional<BACK, int64_t, uint32_t>::type;
-    extern __shared__ uint32_t lds[];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kK4Lds / 4];
     uint8_t *ob = reinterpret_cast<uint8_t *>(lds);  // output ring: position x -> ob[x & M]
-    const uint32_t M = ring - 1;
+    constexpr uint32_t ring = kK4Ring, M = ring - 1;
+    uint32_t *const map32 = lds + ring / 4;          // the batch's element starts, 32 dwords
+    uint16_t *const map16 = reinterpret_cast<uint16_t *>(map32);
     const uint32_t lane = threadIdx.x;
     const uint64_t ix0 = offsets[u], ix1 = offsets[u + 1];
     // comp is 4-byte aligned; the stream starts `bias` bytes into it
@@ -1559,7 +1561,7 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     // copies may reach this far before the unit start
     const uint32_t back_lim = (uint32_t)(base < 0xFFFFFFFFull ? base : 0xFFFFFFFFull);
     // pass 1 re-reads the tail element's position from LDS (past the ring) on its rare path
-    volatile uint32_t *tail_lds = lds + ring / 4;
+    volatile uint32_t *tail_lds = lds + (ring + kK4MapBits / 8) / 4;
     if (!BACK && lane == 0) {
         tail_lds[0] = tail_ip;
         tail_lds[1] = want - skip1;
@@ -1571,7 +1573,7 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     // 512 bytes from the absolute 4-aligned base B: its first 256 in slot ws, the
     // next in slot (ws + 1) % 3; the segment after that is prefetched into `pre`
     // (a register) and written to the free slot when the window slides.
-    auto *const wb = (__attribute__((address_space(3))) uint8_t *)(lds + ring / 4 + 4);
+    auto *const wb = (__attribute__((address_space(3))) uint8_t *)(lds + (ring + kK4MapBits / 8) / 4 + 4);
     auto *const w32 = reinterpret_cast<__attribute__((address_space(3))) uint32_t *>(wb);
     uint64_t B = c0 & ~3ull;
     c1 = c0 + clen;
@@ -1706,35 +1708,34 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             size = t == 0 ? 1 + k + lv + 1 : (t == 1 ? 2 : (t == 2 ? 3 : 5));
         }
         K4STAMP(tb);
-        // ---- element chain from lane 0 by pointer doubling: J^k(0) for lane k
-        uint32_t nx = lane + (size < 64 ? size : 64);  // >= 64: leaves the window
-#define JUMP(T, idx) ({ const uint32_t _i = (idx);                                                   \
-        const uint32_t _g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_i & 63) << 2), (int)(T));    \
-        _i < 64 ? _g : _i; })
-        const uint32_t J1 = nx;
+        // ---- element chain from lane 0 by pointer doubling: J^k(0) for lane k.
+        // Positions are kept as ds_bpermute addresses (4 x position); one >= 256
+        // has left the window: its bpermute result is discarded, so no masking
+        const uint32_t J1 = 4 * lane + 4 * (size < 64 ? size : 64);
+#define JUMP(T, a) ({ const uint32_t _a = (a);                                            \
+        const uint32_t _g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)_a, (int)(T));     \
+        _a < 256 ? _g : _a; })
         const uint32_t J2 = JUMP(J1, J1);
         const uint32_t J4 = JUMP(J2, J2);
         const uint32_t J8 = JUMP(J4, J4);
         const uint32_t J16 = JUMP(J8, J8);
         // (bpermute must run with every lane active: select afterwards).  An
         // element is at least 2 bytes, so 64 positions hold at most 32
-        // elements: lanes >= 32 are out of the batch
-        uint32_t pos = 0;
-        { const uint32_t g = JUMP(J1, pos); pos = (lane & 1) ? g : pos; }
-        { const uint32_t g = JUMP(J2, pos); pos = (lane & 2) ? g : pos; }
-        { const uint32_t g = JUMP(J4, pos); pos = (lane & 4) ? g : pos; }
-        { const uint32_t g = JUMP(J8, pos); pos = (lane & 8) ? g : pos; }
-        { const uint32_t g = JUMP(J16, pos); pos = (lane & 16) ? g : pos; }
-        pos = lane < 32 ? pos : 64;
+        // elements: lanes >= 32 (copies of lanes 0-31) are out of the batch
+        uint32_t pos4 = 0;
+        { const uint32_t g = JUMP(J1, pos4); pos4 = (lane & 1) ? g : pos4; }
+        { const uint32_t g = JUMP(J2, pos4); pos4 = (lane & 2) ? g : pos4; }
+        { const uint32_t g = JUMP(J4, pos4); pos4 = (lane & 4) ? g : pos4; }
+        { const uint32_t g = JUMP(J8, pos4); pos4 = (lane & 8) ? g : pos4; }
+        { const uint32_t g = JUMP(J16, pos4); pos4 = (lane & 16) ? g : pos4; }
 #undef JUMP
-        // lane k < E holds element k of the batch (starts are increasing)
-        const uint64_t inwin = __ballot(pos < 64);
-        uint32_t E = (uint32_t)__builtin_popcountll(inwin);
-        const uint32_t pg = pos < 64 ? pos : 0;
-        const uint32_t e_t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pg << 2), (int)t);
-        const uint32_t e_size = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pg << 2), (int)size);
-        uint32_t e_len = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pg << 2), (int)olen);
-        const uint32_t e_info = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pg << 2), (int)info);
+        // lane k < E holds element k of the batch (starts are increasing);
+        // lanes >= E gather garbage, masked by `live` / nexec below
+        uint32_t E = (uint32_t)__builtin_popcountll(__ballot(pos4 < 256) & 0xFFFFFFFFull);
+        const uint32_t e_t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)pos4, (int)t);
+        const uint32_t e_size = (uint32_t)__builtin_amdgcn_ds_bpermute((int)pos4, (int)size);
+        uint32_t e_len = (uint32_t)__builtin_amdgcn_ds_bpermute((int)pos4, (int)olen);
+        const uint32_t e_info = (uint32_t)__builtin_amdgcn_ds_bpermute((int)pos4, (int)info);
         // exclusive prefix sums of compressed sizes and output lengths over
         // the batch (64-bit safe: garbage past E is zeroed)
         const bool live = lane < E;
@@ -1818,9 +1819,11 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
         // copy byte whose source lies in the same pass waits for the sub-pass
         // that wrote it (out[op+j] = out[op-off + j mod off], :273-280).
         if (nexec && !(longm && (longm & 1))) {
-            // the ring must hold [F, op_end): cut the batch (never below one element)
-            const uint64_t over = __ballot(ring < want && lane < nexec && lane > 0 &&
-                                           op + out_off + e_len - F > ring - 64);
+            // the ring must hold [F, op_end) and the bitmap the batch's output:
+            // cut the batch (never below one element: the first is <= 508 bytes)
+            const uint64_t over = __ballot(lane < nexec && lane > 0 &&
+                                           ((ring < want && op + out_off + e_len - F > ring - 64) ||
+                                            out_off + e_len > kK4MapBits));
             if (over) nexec = (uint32_t)__builtin_ctzll(over);
             if constexpr (BACK) {
                 // copies reading earlier units: wait until those bytes are in HBM
@@ -1851,94 +1854,92 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             // ring slots below lo were overwritten (or are being): read those from HBM
             const uint32_t lo = op_end > ring ? op_end - ring : 0;
             const bool ex = lane < nexec;
+            // the batch's element starts as a bitmap over [op, op_end): bit j of
+            // dword j / 32 = an element starts at op + j (out_off < kK4MapBits, see
+            // `over`); lane w < 32 keeps dword w, pass i reads dwords 2i, 2i + 1
+            map16[lane] = 0;
+            if (ex) __hip_atomic_fetch_or(map32 + (out_off >> 5), 1u << (out_off & 31), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t bm = map32[lane & 31];
+            // element k: kop = output start | literal flag (bit 31); kinfo = the
+            // copy offset, or for a literal its window address (slot base + data
+            // start) + 2^31, so that kinfo + (o - kop) is byte o's window address
             const uint32_t kop = e_op | (e_t == 0 ? 0x80000000u : 0u);
-            const uint32_t kinfo = e_t == 0 ? e_lsrc : e_info;
-            // pass P, first half: which element each byte lane belongs to and
-            // everything that does not read the ring -- the byte's source
-            // position, or its value when it is a literal byte (register
-            // window) or a far copy byte (HBM); pw = value | direct << 8 | pend << 9
-            auto lookup = [&](uint32_t P, SrcT &src, uint32_t &pw) {
-                const uint32_t j = e_op - P;
-                const bool inw = ex && j < 64;
-                const uint32_t cb = (uint32_t)__builtin_popcountll(__ballot(ex && e_op < P));
-                // the pass's element starts as a lane mask: the element lanes are
-                // reversed around cb so that the pass's elements are the highest
-                // lanes (every other lane sends 0, and ds_permute keeps the highest
-                // sender of a collision and gives 0 to lanes nobody targets), then
-                // each element sends 1 to the byte lane where it starts; a byte's
-                // element = the elements before the pass + the starts at or below it
-                const uint32_t pk = (j & 63) | (inw ? 0x100u : 0u);
-                const uint32_t rv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((cb + 63 - lane) & 63) << 2), (int)pk);
-                const uint32_t fl = (uint32_t)__builtin_amdgcn_ds_permute((int)((rv & 63) << 2), (int)(rv >> 8));
-                const uint64_t sm = __ballot(fl != 0);
-                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
-                const uint32_t id = cb + below + (fl != 0 ? 1u : 0u) - 1;
-                const uint32_t f_op = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((id & 63) << 2), (int)kop);
-                const uint32_t f_in = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((id & 63) << 2), (int)kinfo);
+            const uint32_t kinfo = e_t == 0 ? (256 * ws + e_lsrc) ^ 0x80000000u : e_info;
+            uint32_t cb = 0;  // elements starting before the pass
+            // pass P: byte lane l writes output byte o = P + l
+            for (uint32_t P = op, i = 0; P < op_end; P += 64, i++) {
+                const uint64_t sm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(bm, 2 * i + 1) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane(bm, 2 * i);
+                // the byte's element: cb - 1 + the starts in [P, P + l] (the first
+                // pass starts with one, so it is never -1)
+                const uint64_t sm1 = sm >> 1;
+                const uint32_t id = __builtin_amdgcn_mbcnt_hi(
+                    (uint32_t)(sm1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm1, cb - 1 + (uint32_t)(sm & 1)));
+                cb += (uint32_t)__builtin_popcountll(sm);
+                const uint32_t f_op = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)kop);
+                const uint32_t f_in = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)kinfo);
                 const uint32_t o = P + lane;
-                const bool lit = (f_op >> 31) != 0;
-                uint32_t d = o - (f_op & 0x7FFFFFFFu);
-                // a far source (below lo: only in HBM) never overlaps its copy (off >
-                // ring - 64 > len): its load is issued before the window gather
-                const SrcT src0 = (SrcT)(f_op & 0x7FFFFFFFu) - (SrcT)f_in + (SrcT)d;
-                bool farl = !lit && o < op_end && src0 < (SrcT)lo;
-                uint8_t fv = 0;
-                if (farl) fv = dst[src0];
-                // literal byte from the window (read by every lane: garbage for copies)
-                const uint8_t lb = wb[WADR((f_in + d) & 511)];
-                if (!lit && d >= f_in && f_in) {  // overlapping copy (off < len <= 64)
+                const uint32_t d = o - f_op;  // a literal's carries 2^31, cancelled by its kinfo
+                const bool lit = (int32_t)f_op < 0;
+                const bool pend = o < op_end;
+                // copy source (pass 2: negative = an earlier unit).  Below lo only
+                // HBM holds the byte: a far copy never overlaps (off > ring - 64 >
+                // len), so its load goes out first, into a register of its own
+                SrcT src = (SrcT)o - (SrcT)f_in;
+                bool far = pend && !lit && src < (SrcT)lo;
+                uint32_t fv = 0, lb = 0;
+                if (far) fv = dst[src];
+                // literal byte: the window's LDS copy (3 slots of 256 bytes)
+                if (pend && lit) {
+                    const uint32_t a = f_in + d, a2 = a - 768;
+                    lb = wb[a < a2 ? a : a2];
+                }
+                if (pend && !lit && !far && d >= f_in) {
+                    // overlapping copy (off < len <= 64): source byte d mod off
                     const float r = __builtin_amdgcn_rcpf((float)f_in);
                     const uint32_t qd = (uint32_t)((float)d * r + 0.0001f);
-                    d -= qd * f_in;
-                }
-                src = (SrcT)(f_op & 0x7FFFFFFFu) - (SrcT)f_in + (SrcT)d;
-                const bool pend = o < op_end;
-                if constexpr (BACK) {
-                    // an overlapping copy near the unit start may repeat bytes of an earlier unit
-                    if (!lit && pend && !farl && src < (SrcT)lo) {
-                        fv = dst[src];
-                        farl = true;
+                    src = (SrcT)f_op - (SrcT)f_in + (SrcT)(d - qd * f_in);
+                    if constexpr (BACK) {
+                        // near the unit start it may repeat bytes of an earlier unit
+                        if (src < (SrcT)lo) {
+                            fv = dst[src];
+                            far = true;
+                        }
                     }
                 }
+                const bool direct = lit || far;
 #ifdef SNAPPY_K4_STATS
-                n_far += __ballot(farl) != 0;
-#endif
-                pw = (uint32_t)(lit ? lb : fv) | ((lit || farl) ? 0x100u : 0u) | (pend ? 0x200u : 0u);
-            };
-            // pass P, second half: the ring
-            auto execute = [&](uint32_t P, SrcT src, uint32_t pw) {
-                const uint32_t o = P + lane;
-                const bool direct = (pw & 0x100u) != 0;
-                bool pend = (pw & 0x200u) != 0;
-#ifdef SNAPPY_K4_STATS
+                n_far += __ballot(pend && !lit && direct) != 0;
                 n_pass++;
 #endif
+                const bool near = pend && !direct;  // reads the ring
                 // the common pass: no byte depends on another byte of the same pass
-                if (!__ballot(pend && !direct && src >= (SrcT)P)) {
-                    if (pend) ob[o & M] = direct ? (uint8_t)pw : ob[(uint32_t)src & M];
+                // (the ring read goes out before the far load is waited for)
+                if (!__ballot(near && src >= (SrcT)P)) {
+                    uint32_t rv = 0;
+                    if (near) rv = ob[(uint32_t)src & M];
+                    if (pend) ob[o & M] = (uint8_t)(lit ? lb : (far ? fv : rv));
 #ifdef SNAPPY_K4_STATS
                     n_sub++;
 #endif
-                    return;
+                    continue;
                 }
                 // else sub-passes: a byte is written once its source byte has been
+                // (out[op+j] = out[op-off + j mod off], :273-280)
+                const uint32_t v = lit ? lb : fv;  // a direct byte's value
                 uint64_t written = 0;
+                bool pd = pend;
                 for (;;) {
-                    const bool rdy = pend && (direct || src < (SrcT)P || ((written >> ((uint32_t)(src - (SrcT)P) & 63)) & 1));
-                    if (rdy) ob[o & M] = direct ? (uint8_t)pw : ob[(uint32_t)src & M];
+                    const bool rdy = pd && (direct || src < (SrcT)P || ((written >> ((uint32_t)(src - (SrcT)P) & 63)) & 1));
+                    if (rdy) ob[o & M] = direct ? (uint8_t)v : ob[(uint32_t)src & M];
                     written |= __ballot(rdy);
-                    pend = pend && !rdy;
+                    pd = pd && !rdy;
 #ifdef SNAPPY_K4_STATS
                     n_sub++;
 #endif
-                    if (!__ballot(pend)) break;
+                    if (!__ballot(pd)) break;
                 }
-            };
-            for (uint32_t P = op; P < op_end; P += 64) {
-                SrcT sa;
-                uint32_t wa;
-                lookup(P, sa, wa);
-                execute(P, sa, wa);
             }
         }
         K4STAMP(td);
@@ -1993,10 +1994,10 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
 #if SNAPPY_TU_DECODE
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_decompress_units(
     const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets, uint64_t n, uint32_t unit,
-    uint32_t hdr_mode, uint64_t header_value, uint32_t ring, uint32_t allow_back, uint32_t bias, uint8_t *__restrict__ out,
+    uint32_t hdr_mode, uint64_t header_value, uint32_t allow_back, uint32_t bias, uint8_t *__restrict__ out,
     int32_t *__restrict__ status)
 {
-    k4_body<false>(comp, offsets, n, unit, hdr_mode, header_value, ring, allow_back, bias, out, status, blockIdx.x);
+    k4_body<false>(comp, offsets, n, unit, hdr_mode, header_value, allow_back, bias, out, status, blockIdx.x);
 }
 #endif
 
@@ -2004,7 +2005,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_de
 __global__ __launch_bounds__(64) void k4_decompress_back(const uint8_t *__restrict__ comp,
                                                          const uint64_t *__restrict__ offsets, uint64_t n,
                                                          uint32_t unit, uint32_t hdr_mode, uint64_t header_value,
-                                                         uint32_t ring, uint32_t bias, uint8_t *__restrict__ out,
+                                                         uint32_t bias, uint8_t *__restrict__ out,
                                                          int32_t *__restrict__ status)
 {
     // status[units + 1] == 0: pass 1 deferred nothing (the common case: every wave leaves at once)
@@ -2014,7 +2015,7 @@ __global__ __launch_bounds__(64) void k4_decompress_back(const uint8_t *__restri
     if (threadIdx.x == 0) tk = atomicAdd(reinterpret_cast<uint32_t *>(status + gridDim.x), 1u);
     const uint32_t u = __builtin_amdgcn_readfirstlane(tk);
     if (status[u] != SNAPPY_ST_DEFER) return;
-    k4_body<true>(comp, offsets, n, unit, hdr_mode, header_value, ring, 1u, bias, out, status, u);
+    k4_body<true>(comp, offsets, n, unit, hdr_mode, header_value, 1u, bias, out, status, u);
 }
 #endif
 // ---------------------------------------------------------------------------

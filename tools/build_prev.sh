@@ -3,8 +3,9 @@
 # lightweight-snappy_amd/variants/libsnappy_amd_<name>.so (default name: prev)
 # for A/B against the working tree with tools/variant_bench.py.  Same
 # compile flags as the Makefile (compress kernels with the compress
-# scheduler, decode kernels with max-ilp); host code from the working tree.
-#   tools/build_prev.sh [REV] [NAME] [extra -D flags...]
+# scheduler, decode kernels with max-ilp); kernels + device shim from REV,
+# the C host code from the working tree.
+#   tools/build_prev.sh [REV|WORK|DIR:path] [NAME] [extra -D flags...]
 set -e
 cd "$(dirname "$0")/.."
 REV=${1:-HEAD}
@@ -12,16 +13,25 @@ NAME=${2:-prev}
 shift 2 2>/dev/null || shift $#
 P=lightweight-snappy_amd
 mkdir -p $P/variants $P/build
-SRC=$P/csrc/.${NAME}_kernels.hip
-if [ "$REV" = "WORK" ]; then cp $P/csrc/snappy_kernels.hip $SRC; else git show $REV:$P/csrc/snappy_kernels.hip > $SRC; fi
-trap 'rm -f $SRC' EXIT
-FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -Iinclude -I$P/csrc $*"
+# the kernels, their private header and the device shim from REV (the
+# shim launches the kernels with REV's signatures); the C host from the tree
+D=$P/build/src_$NAME
+rm -rf $D && mkdir -p $D
+for f in snappy_kernels.hip snappy_kernels.h snappy_device.hip; do
+    case $REV in
+    WORK) cp $P/csrc/$f $D/$f ;;
+    DIR:*) cp ${REV#DIR:}/$f $D/$f ;;  # a directory holding the three files
+    *) git show $REV:$P/csrc/$f > $D/$f ;;
+    esac
+done
+FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -Iinclude -I$D $*"
 SC="-mllvm -amdgpu-sched-strategy=max-memory-clause -mllvm -amdgpu-use-amdgpu-trackers"
 SD="-mllvm -amdgpu-sched-strategy=max-ilp"
-hipcc $FLAGS $SC -DSNAPPY_TU=1 -x hip -c $SRC -o $P/build/kc_$NAME.o
-hipcc $FLAGS $SD -DSNAPPY_TU=2 -x hip -c $SRC -o $P/build/kd_$NAME.o
-hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -Iinclude -I$P/csrc -c $P/csrc/snappy_device.hip -o $P/build/dev_var.o
+hipcc $FLAGS $SC -DSNAPPY_TU=1 -x hip -c $D/snappy_kernels.hip -o $P/build/kc_$NAME.o
+hipcc $FLAGS $SD -DSNAPPY_TU=2 -x hip -c $D/snappy_kernels.hip -o $P/build/kd_$NAME.o
+hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -Iinclude -I$D -c $D/snappy_device.hip -o $P/build/dev_$NAME.o
 gcc -O2 -fPIC -std=gnu11 -Iinclude -c $P/csrc/snappy_host.c -o $P/build/host_var.o
 hipcc --offload-arch=gfx950 -shared -fPIC -o $P/variants/libsnappy_amd_$NAME.so $P/build/kc_$NAME.o $P/build/kd_$NAME.o \
-    $P/build/dev_var.o $P/build/host_var.o
+    $P/build/dev_$NAME.o $P/build/host_var.o
+rm -rf $D
 echo "built $NAME ($REV $*)"

@@ -32,14 +32,21 @@ for step in "$@"; do
     ab:*)  # ab:<variant,variant,...>:<kind>:<chunk>:<layout> -> tools/variant_bench.py, 1 GiB
         IFS=: read -r _ vs kind chunk layout <<< "$step"
         timeout -k 10 400 python -u tools/variant_bench.py ${vs//,/ } --kind $kind --n 1073741824 --chunk $chunk \
-            --layout $layout --reps 3 --rounds 2 > "$out/ab_${kind}_${chunk}.log" 2>&1
-        rc=$?; echo "ab rc=$rc"; tail -6 "$out/ab_${kind}_${chunk}.log"; [ $rc -ne 0 ] && exit $rc ;;
+            --layout $layout --reps 3 --rounds 2 > "$out/ab_${vs//,/-}_${kind}_${chunk}.log" 2>&1
+        rc=$?; echo "ab rc=$rc"; tail -6 "$out/ab_${vs//,/-}_${kind}_${chunk}.log"; [ $rc -ne 0 ] && exit $rc ;;
     pmc:*)  # pmc:<tag>:<workload>:<COUNTER,COUNTER,...> -> one rocprofv3 counter pass over a 1-step bench
         IFS=: read -r _ tag wl ctrs <<< "$step"
         timeout -s KILL 240 rocprofv3 --pmc ${ctrs//,/ } --kernel-trace -d "$out/pmc_$tag" -o run \
             --output-format csv -- python3 bench.py --workload $wl --steps 1 --warmup 1 --no-cpu-baseline \
             --no-host-e2e --no-sub > "$out/pmc_$tag.log" 2>&1
         rc=$?; echo "pmc $tag rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
+    pmcv:*)  # pmcv:<variant>:<tag>:<workload>:<COUNTERS> -> the same pass over variants/libsnappy_amd_<variant>.so
+        IFS=: read -r _ var tag wl ctrs <<< "$step"
+        SNAPPY_AMD_LIB=$PWD/lightweight-snappy_amd/variants/libsnappy_amd_$var.so \
+            timeout -s KILL 240 rocprofv3 --pmc ${ctrs//,/ } --kernel-trace -d "$out/pmc_$tag" -o run \
+            --output-format csv -- python3 bench.py --workload $wl --steps 1 --warmup 1 --no-cpu-baseline \
+            --no-host-e2e --no-sub > "$out/pmc_$tag.log" 2>&1
+        rc=$?; echo "pmcv $tag rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
     counters)
         timeout -k 10 120 rocprofv3 --list-avail > "$out/counters.txt" 2>&1
         rc=$?; echo "counters rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
@@ -49,6 +56,12 @@ for step in "$@"; do
             SNAPPY_K1R_DYNLDS=$d timeout -k 10 200 python -u tools/k1r_stats.py $kind 268435456 $chunk \
                 > "$out/occ_${kind}_${chunk}_$d.log" 2>&1
             rc=$?; echo "occ $d rc=$rc"; cat "$out/occ_${kind}_${chunk}_$d.log"; [ $rc -ne 0 ] && exit $rc
+        done ;;
+    k4s:*)  # k4s:<variant,...>:<kind> -> K4 statistics builds (SNAPPY_K4_STATS), 256 MiB of 32 KiB streams
+        IFS=: read -r _ vs kind <<< "$step"
+        for v in ${vs//,/ }; do
+            timeout -k 10 200 python -u tools/k4_stats.py $kind 268435456 $v > "$out/k4s_${v}_$kind.log" 2>&1
+            rc=$?; echo "k4s $v rc=$rc"; cat "$out/k4s_${v}_$kind.log"; [ $rc -ne 0 ] && exit $rc
         done ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""Cycles per element of K4 (SNAPPY_K4_STATS build)."""
+"""Cycles per element of K4 (SNAPPY_K4_STATS build).
+Usage: tools/k4_stats.py KIND BYTES [VARIANT]  (variants/libsnappy_amd_<VARIANT>.so, default k4stats)"""
 import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "lightweight-snappy_amd"))
-os.environ["SNAPPY_AMD_LIB"] = os.path.join(ROOT, "lightweight-snappy_amd", "variants", "libsnappy_amd_k4stats.so")
+os.environ["SNAPPY_AMD_LIB"] = os.path.join(ROOT, "lightweight-snappy_amd", "variants", f"libsnappy_amd_{sys.argv[3] if len(sys.argv) > 3 else 'k4stats'}.so")
 import numpy as np, torch
 import datagen, snappy_amd
 kind = sys.argv[1]; n = int(sys.argv[2]); chunk = 32768

@@ -1517,7 +1517,8 @@ static __device__ uint64_t g_k4_stats[8];  // (k4_body is parsed, never instanti
 // output ring, the batch's element-start bitmap, two scalars, the window
 constexpr uint32_t kK4Ring = 4096;    // output ring; copies reaching further back read HBM
 constexpr uint32_t kK4MapBits = 1024; // a batch's output span (bit j = an element starts at op + j)
-constexpr uint32_t kK4Lds = kK4Ring + kK4MapBits / 8 + 16 + 784;  // 5,024 B: 32 waves per CU fit 160 KiB
+constexpr uint32_t kK4Dummy = kK4Ring + kK4MapBits / 8 + 16 + 784;  // a byte lanes past a pass's end write
+constexpr uint32_t kK4Lds = kK4Dummy + 4;  // 5,028 B: 32 waves per CU fit 160 KiB
 
 template <bool BACK>
 __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets,
@@ -1692,20 +1693,28 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
         // two aligned dwords (one ds_read2_b32; unaligned LDS reads measured slower)
         const uint32_t dA = w32[qa >> 2], dB = w32[(qa >> 2) + 1];
         const uint32_t sh = 8 * (qa & 3);
-        const uint32_t x0 = sh ? (dA >> sh) | (dB << (32 - sh)) : dA;  // tag, t1, t2, t3
+        const uint32_t x0 = __builtin_amdgcn_alignbit(dB, dA, sh);  // tag, t1, t2, t3 (sh = 0: dA)
         const uint32_t x1 = dB >> sh;  // t4 in bits 0..7 (the only byte used: b4 below)
         const uint32_t tag = x0 & 0xFF;
         uint32_t size, olen, info;  // info: copy offset, or literal header length
         const uint32_t t = tag & 3;
-        {  // branch-free tag dispatch (src/snappy_decompression.c:290-333)
+        {  // tag dispatch in selects of precomputed values (no exec-mask branches;
+           // src/snappy_decompression.c:290-333)
             const uint32_t m = tag >> 2;
-            const uint32_t k = m >= 60 ? m - 59 : 0;  // literal: extra length bytes
-            const uint32_t b4 = (x0 >> 8) | (x1 << 24);
-            const uint32_t lv = k == 0 ? m : (k == 4 ? b4 : (x0 >> 8) & ((1u << (8 * (k & 3))) - 1));
-            const uint32_t c1b = ((tag >> 5) << 8) | ((x0 >> 8) & 0xFF);
-            olen = t == 0 ? lv + 1 : (t == 1 ? (m & 7) + 4 : m + 1);  // garbage lengths are clamped below
-            info = t == 0 ? 1 + k : (t == 1 ? c1b : (t == 2 ? (x0 >> 8) & 0xFFFF : b4));
-            size = t == 0 ? 1 + k + lv + 1 : (t == 1 ? 2 : (t == 2 ? 3 : 5));
+            const uint32_t b4 = __builtin_amdgcn_alignbit(x1, x0, 8);  // bytes 1..4
+            const uint32_t k = __builtin_elementwise_sub_sat(m, 59u);  // literal: extra length bytes
+            const uint32_t lx = b4 & (0xFFFFFFFFu >> ((32 - 8 * k) & 31));
+            const uint32_t lv = k ? lx : m;
+            const uint32_t l_olen = lv + 1, c1_olen = (m & 7) + 4, c_olen = m + 1;
+            const uint32_t c1b = ((tag >> 5) << 8) | (b4 & 0xFF), c2b = b4 & 0xFFFF, l_info = 1 + k;
+            const uint32_t l_size = lv + k + 2, c_size = (0x5320u >> (4 * t)) & 0xF;  // copies: 2, 3, 5 bytes
+            const bool is_l = t == 0, is_c1 = t == 1, is_c2 = t == 2;
+            const uint32_t cx_olen = is_c1 ? c1_olen : c_olen;
+            olen = is_l ? l_olen : cx_olen;  // garbage lengths are clamped below
+            const uint32_t c24 = is_c2 ? c2b : b4;
+            const uint32_t cx_info = is_c1 ? c1b : c24;
+            info = is_l ? l_info : cx_info;
+            size = is_l ? l_size : c_size;
         }
         K4STAMP(tb);
         // ---- element chain from lane 0 by pointer doubling: J^k(0) for lane k.
@@ -1765,10 +1774,15 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 }
             }
         } else {
-            if (e_op >= want) e_err = 1;  // done before this element: not an error
-            else if (e_size > clen - e_ip) e_err = SNAPPY_ST_TRUNCATED;
-            else if (e_t != 0 && (e_info == 0 || e_info > e_op)) e_err = e_info ? SNAPPY_ST_DEFER : SNAPPY_ST_OFFSET;
-            else if (e_len > want - e_op) e_err = kK4Tail;
+            // (selects of precomputed conditions, not exec-mask branches)
+            const bool done = e_op >= want;  // done before this element: not an error
+            const bool trunc = e_size > clen - e_ip;
+            const bool back = e_t != 0 && e_info - 1 >= e_op;  // offset 0, or reaching before the unit
+            const int32_t back_err = e_info ? SNAPPY_ST_DEFER : SNAPPY_ST_OFFSET;
+            const int32_t tail_err = e_len > want - e_op ? kK4Tail : SNAPPY_ST_OK;
+            const int32_t e3 = back ? back_err : tail_err;
+            const int32_t e2 = trunc ? SNAPPY_ST_TRUNCATED : e3;
+            e_err = done ? 1 : e2;
         }
         const uint64_t badm = __ballot(live && e_err != SNAPPY_ST_OK);
         uint32_t nexec = E;
@@ -1888,13 +1902,16 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 // len), so its load goes out first, into a register of its own
                 SrcT src = (SrcT)o - (SrcT)f_in;
                 bool far = pend && !lit && src < (SrcT)lo;
-                uint32_t fv = 0, lb = 0;
+                uint32_t fv = 0;
+#ifndef SNAPPY_K4_NOFAR  // (experiment only: wrong output, measures what the far loads cost)
                 if (far) fv = dst[src];
-                // literal byte: the window's LDS copy (3 slots of 256 bytes)
-                if (pend && lit) {
-                    const uint32_t a = f_in + d, a2 = a - 768;
-                    lb = wb[a < a2 ? a : a2];
-                }
+#endif
+                // literal byte: the window's LDS copy (3 slots of 256 bytes), read
+                // by every lane (no exec change): a copy lane's address is clamped
+                uint32_t a = f_in + d;
+                const uint32_t a2 = a - 768;
+                a = a < a2 ? a : a2;
+                const uint32_t lb = wb[a < 783 ? a : 783];
                 if (pend && !lit && !far && d >= f_in) {
                     // overlapping copy (off < len <= 64): source byte d mod off
                     const float r = __builtin_amdgcn_rcpf((float)f_in);
@@ -1917,9 +1934,10 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 // the common pass: no byte depends on another byte of the same pass
                 // (the ring read goes out before the far load is waited for)
                 if (!__ballot(near && src >= (SrcT)P)) {
-                    uint32_t rv = 0;
-                    if (near) rv = ob[(uint32_t)src & M];
-                    if (pend) ob[o & M] = (uint8_t)(lit ? lb : (far ? fv : rv));
+                    // every lane reads the ring and writes (a lane past op_end to the
+                    // dummy byte after the window): no exec changes
+                    const uint32_t rv = ob[(uint32_t)src & M];
+                    ob[pend ? (o & M) : kK4Dummy] = (uint8_t)(lit ? lb : (far ? fv : rv));
 #ifdef SNAPPY_K4_STATS
                     n_sub++;
 #endif

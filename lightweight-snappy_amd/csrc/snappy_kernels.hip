@@ -1416,6 +1416,14 @@ __device__ __forceinline__ uint32_t load_dw_guarded(const uint8_t *comp, uint64_
     return w;
 }
 
+// lane l <- dword l of the 256-byte segment at a0 (4-aligned): one uniform test
+// instead of a per-lane 64-bit bound check unless the segment reaches lim
+__device__ __forceinline__ uint32_t load_seg(const uint8_t *comp, uint64_t a0, uint64_t lim, uint32_t lane)
+{
+    if (a0 + 256 <= lim) return __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(comp + a0) + lane);
+    return load_dw_guarded(comp, a0 + 4 * lane, lim);
+}
+
 // ring -> HBM for output bytes [F, T): 16-byte stores on a 16-aligned
 // destination, bytes otherwise
 __device__ __forceinline__ void k4_flush(const uint8_t *ob, uint32_t M, uint8_t *dst, uint32_t F, uint32_t T,
@@ -1513,12 +1521,15 @@ static __device__ uint64_t g_k4_stats[8];  // (k4_body is parsed, never instanti
 #define K4STAMP(var) do { } while (0)
 #endif
 
-// K4's LDS (static, so every base folds into the ds offset field): the
-// output ring, the batch's element-start bitmap, two scalars, the window
+// K4's LDS (static, so every base folds into a ds offset field): the
+// compressed window at 0 (ds_read2 has only 8-bit dword offsets), the batch's
+// element-start bitmap, two scalars, the output ring and one dummy byte
 constexpr uint32_t kK4Ring = 4096;    // output ring; copies reaching further back read HBM
 constexpr uint32_t kK4MapBits = 1024; // a batch's output span (bit j = an element starts at op + j)
-constexpr uint32_t kK4Dummy = kK4Ring + kK4MapBits / 8 + 16 + 784;  // a byte lanes past a pass's end write
-constexpr uint32_t kK4Lds = kK4Dummy + 4;  // 5,028 B: 32 waves per CU fit 160 KiB
+constexpr uint32_t kK4MapAt = 784;    // after the window: 3 x 256 bytes + a 16-byte mirror
+constexpr uint32_t kK4TailAt = kK4MapAt + kK4MapBits / 8;
+constexpr uint32_t kK4RingAt = kK4TailAt + 16;
+constexpr uint32_t kK4Lds = kK4RingAt + kK4Ring + 4;  // 5,028 B: 32 waves per CU fit 160 KiB
 
 template <bool BACK>
 __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets,
@@ -1529,9 +1540,9 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     // copy source positions: relative to the unit start, negative = an earlier unit (pass 2 only)
     using SrcT = typename std::conditional<BACK, int64_t, uint32_t>::type;
     __shared__ __attribute__((aligned(16))) uint32_t lds[kK4Lds / 4];
-    uint8_t *ob = reinterpret_cast<uint8_t *>(lds);  // output ring: position x -> ob[x & M]
+    uint8_t *ob = reinterpret_cast<uint8_t *>(lds + kK4RingAt / 4);  // output ring: position x -> ob[x & M]
     constexpr uint32_t ring = kK4Ring, M = ring - 1;
-    uint32_t *const map32 = lds + ring / 4;          // the batch's element starts, 32 dwords
+    uint32_t *const map32 = lds + kK4MapAt / 4;      // the batch's element starts, 32 dwords
     uint16_t *const map16 = reinterpret_cast<uint16_t *>(map32);
     const uint32_t lane = threadIdx.x;
     const uint64_t ix0 = offsets[u], ix1 = offsets[u + 1];
@@ -1562,7 +1573,7 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     // copies may reach this far before the unit start
     const uint32_t back_lim = (uint32_t)(base < 0xFFFFFFFFull ? base : 0xFFFFFFFFull);
     // pass 1 re-reads the tail element's position from LDS (past the ring) on its rare path
-    volatile uint32_t *tail_lds = lds + (ring + kK4MapBits / 8) / 4;
+    volatile uint32_t *tail_lds = lds + kK4TailAt / 4;
     if (!BACK && lane == 0) {
         tail_lds[0] = tail_ip;
         tail_lds[1] = want - skip1;
@@ -1574,7 +1585,7 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     // 512 bytes from the absolute 4-aligned base B: its first 256 in slot ws, the
     // next in slot (ws + 1) % 3; the segment after that is prefetched into `pre`
     // (a register) and written to the free slot when the window slides.
-    auto *const wb = (__attribute__((address_space(3))) uint8_t *)(lds + (ring + kK4MapBits / 8) / 4 + 4);
+    auto *const wb = (__attribute__((address_space(3))) uint8_t *)lds;
     auto *const w32 = reinterpret_cast<__attribute__((address_space(3))) uint32_t *>(wb);
     uint64_t B = c0 & ~3ull;
     c1 = c0 + clen;
@@ -1587,9 +1598,9 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     };
     uint32_t pre;
     {
-        const uint32_t w0 = load_dw_guarded(comp, B + 4 * lane, c1);
-        const uint32_t w1 = load_dw_guarded(comp, B + 256 + 4 * lane, c1);
-        pre = load_dw_guarded(comp, B + 512 + 4 * lane, c1);
+        const uint32_t w0 = load_seg(comp, B, c1, lane);
+        const uint32_t w1 = load_seg(comp, B + 256, c1, lane);
+        pre = load_seg(comp, B + 512, c1, lane);
         put_seg(0, w0);
         put_seg(1, w1);
         __builtin_amdgcn_wave_barrier();
@@ -1681,11 +1692,11 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 B = (c0 + ip) & ~3ull;
                 o = (uint32_t)(c0 + ip - B);
                 ws = 0;
-                put_seg(0, load_dw_guarded(comp, B + 4 * lane, c1));
-                put_seg(1, load_dw_guarded(comp, B + 256 + 4 * lane, c1));
+                put_seg(0, load_seg(comp, B, c1, lane));
+                put_seg(1, load_seg(comp, B + 256, c1, lane));
             }
             __builtin_amdgcn_wave_barrier();
-            pre = load_dw_guarded(comp, B + 512 + 4 * lane, c1);
+            pre = load_seg(comp, B + 512, c1, lane);
         }
         // ---- lane-parallel candidate parse: an element starting at o + lane
         const uint32_t q = o + lane;  // < 320
@@ -1930,34 +1941,32 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 n_far += __ballot(pend && !lit && direct) != 0;
                 n_pass++;
 #endif
-                const bool near = pend && !direct;  // reads the ring
-                // the common pass: no byte depends on another byte of the same pass
-                // (the ring read goes out before the far load is waited for)
-                if (!__ballot(near && src >= (SrcT)P)) {
-                    // every lane reads the ring and writes (a lane past op_end to the
-                    // dummy byte after the window): no exec changes
-                    const uint32_t rv = ob[(uint32_t)src & M];
-                    ob[pend ? (o & M) : kK4Dummy] = (uint8_t)(lit ? lb : (far ? fv : rv));
+                // every lane reads the ring (a byte whose source lies in this pass
+                // reads garbage, replaced below) and writes (a lane past op_end to the
+                // dummy byte after the ring): no exec changes
+                const bool inpass = pend && !direct && src >= (SrcT)P;
+                const uint32_t rv = ob[(uint32_t)src & M];
+                uint32_t val = lit ? lb : (far ? fv : rv);
+                if (__builtin_expect(__ballot(inpass) != 0, 0)) {
+                    // out[op+j] = out[op-off + j mod off] (:273-280) with the source in
+                    // this pass: lane src - P (a lower lane) holds it.  Follow those
+                    // links by pointer jumping to a lane whose value is known (direct,
+                    // or read from the ring), then take its value
+                    uint32_t rt = inpass ? (uint32_t)(src - (SrcT)P) : lane;
+                    for (;;) {
 #ifdef SNAPPY_K4_STATS
-                    n_sub++;
+                        n_sub++;
 #endif
-                    continue;
+                        const uint32_t r2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rt << 2), (int)rt);
+                        if (!__ballot(r2 != rt)) break;
+                        rt = r2;
+                    }
+                    val = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rt << 2), (int)val);
                 }
-                // else sub-passes: a byte is written once its source byte has been
-                // (out[op+j] = out[op-off + j mod off], :273-280)
-                const uint32_t v = lit ? lb : fv;  // a direct byte's value
-                uint64_t written = 0;
-                bool pd = pend;
-                for (;;) {
-                    const bool rdy = pd && (direct || src < (SrcT)P || ((written >> ((uint32_t)(src - (SrcT)P) & 63)) & 1));
-                    if (rdy) ob[o & M] = direct ? (uint8_t)v : ob[(uint32_t)src & M];
-                    written |= __ballot(rdy);
-                    pd = pd && !rdy;
+                ob[pend ? (o & M) : kK4Ring] = (uint8_t)val;
 #ifdef SNAPPY_K4_STATS
-                    n_sub++;
+                n_sub++;
 #endif
-                    if (!__ballot(pd)) break;
-                }
             }
         }
         K4STAMP(td);
@@ -2010,7 +2019,10 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
 }
 
 #if SNAPPY_TU_DECODE
-__global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void k4_decompress_units(
+#ifndef SNAPPY_K4_WAVES
+#define SNAPPY_K4_WAVES 8  // waves per SIMD: <= 64 VGPRs, <= 80 SGPRs (5,028 B of LDS: 32 per CU fit)
+#endif
+__global__ __launch_bounds__(64, SNAPPY_K4_WAVES) void k4_decompress_units(
     const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets, uint64_t n, uint32_t unit,
     uint32_t hdr_mode, uint64_t header_value, uint32_t allow_back, uint32_t bias, uint8_t *__restrict__ out,
     int32_t *__restrict__ status)

@@ -1,7 +1,8 @@
 /* Drop-in replacement of src/buffer_compression.h:8-16 (tturturiello/lightweight-snappy):
  * the byte-cursor helpers the reference's block loop is written with.  The MI355X codec
- * keeps its own cursors on the device; these host helpers are exported from
- * libsnappy_amd.so only so that code built against the reference header still links. */
+ * keeps its own cursors on the device; these host helpers live in the separate
+ * libsnappy_amd_compat.so (not libsnappy_amd.so: their generic names could interpose on
+ * an application's symbols), for code built against the reference header. */
 #ifndef SNAPPY_BUFFER_COMPRESSION_H
 #define SNAPPY_BUFFER_COMPRESSION_H
 typedef struct buffer {

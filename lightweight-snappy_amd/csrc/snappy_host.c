@@ -15,7 +15,6 @@
 #include <string.h>
 
 #include "snappy_amd.h"
-#include "buffer_compression.h"
 #include "snappy_amd_internal.h"
 
 static __thread int g_last_status = SNAPPY_AMD_OK;
@@ -188,20 +187,4 @@ int snappy_compress_bst(FILE *file_input, unsigned long long input_size, FILE *f
     g_last_status = SNAPPY_AMD_ERR_UNSUPPORTED;
     return SNAPPY_AMD_ERR_UNSUPPORTED;
 }
-
-/* ---- reference Buffer cursor helpers (include/buffer_compression.h) ---- */
-void init_Buffer(Buffer *bf, unsigned int buffer_size)
-{
-    char *p = (char *)calloc(buffer_size ? buffer_size : 1, 1);
-    bf->beginning = bf->current = p;
-    bf->bytes_left = p ? buffer_size : 0;
-}
-
-void move_current(Buffer *bf, unsigned int offset)
-{
-    bf->current += offset;
-    bf->bytes_left -= offset;
-}
-
-void reset(Buffer *bf) { bf->current = bf->beginning; }
 

@@ -108,11 +108,15 @@ _SIGS = {
                                                  _c.POINTER(_c.c_uint64)]),
     # FILE* in, sidecar entries (or NULL) and their count, FILE* out
     "snappy_amd_host_decompress_file": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_void_p]),
-    # reference Buffer cursor helpers (Buffer* is a struct of two pointers and a u32)
+}
+# the reference Buffer cursor helpers, in libsnappy_amd_compat.so (Buffer* is a
+# struct of two pointers and a u32)
+_COMPAT_SIGS = {
     "init_Buffer": (None, [_c.c_void_p, _c.c_uint]),
     "move_current": (None, [_c.c_void_p, _c.c_uint]),
     "reset": (None, [_c.c_void_p]),
 }
+COMPAT_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsnappy_amd_compat.so")
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -137,6 +141,18 @@ def lib() -> ctypes.CDLL:
             fn.argtypes = args
         _lib = l
     return _lib
+
+
+def compat_lib() -> ctypes.CDLL:
+    """Load libsnappy_amd_compat.so (the reference's Buffer cursor helpers)."""
+    if not os.path.exists(COMPAT_PATH):
+        raise RuntimeError(f"{COMPAT_PATH} is missing: run __graft_entry__.build()")
+    l = ctypes.CDLL(COMPAT_PATH)
+    for name, (res, args) in _COMPAT_SIGS.items():
+        fn = getattr(l, name)
+        fn.restype = res
+        fn.argtypes = args
+    return l
 
 
 def _check(rc: int, what: str) -> None:

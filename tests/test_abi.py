@@ -14,10 +14,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 INC = os.path.join(ROOT, "include")
 
 
-def declared_functions():
+COMPAT_HEADERS = ("buffer_compression.h",)  # exported by libsnappy_amd_compat.so instead
+
+
+def declared_functions(compat=False):
     names = set()
     for h in os.listdir(INC):
-        if not h.endswith(".h"):
+        if not h.endswith(".h") or (h in COMPAT_HEADERS) != compat:
             continue
         src = open(os.path.join(INC, h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
@@ -44,6 +47,19 @@ def test_library_exports_every_declared_symbol():
 
 def test_python_binding_covers_header():
     assert declared_functions() <= set(snappy_amd._SIGS)
+    assert declared_functions(compat=True) <= set(snappy_amd._COMPAT_SIGS)
+
+
+def test_compat_library_holds_the_generic_names():
+    # init_Buffer / move_current / reset: in libsnappy_amd_compat.so only, so
+    # linking the codec cannot interpose on an application's own `reset`
+    names = declared_functions(compat=True)
+    assert names == {"init_Buffer", "move_current", "reset"}
+    main = subprocess.run(["nm", "-D", "--defined-only", snappy_amd.LIB_PATH], capture_output=True, text=True).stdout
+    comp = subprocess.run(["nm", "-D", "--defined-only", snappy_amd.COMPAT_PATH], capture_output=True, text=True).stdout
+    for n in names:
+        assert not re.search(rf"\b{n}$", main, flags=re.M), n
+        assert re.search(rf"\bT {n}$", comp, flags=re.M), n
 
 
 def test_varint_host(golden):
@@ -94,7 +110,7 @@ def test_buffer_cursor_helpers():
     class Buffer(ctypes.Structure):
         _fields_ = [("current", ctypes.c_void_p), ("beginning", ctypes.c_void_p), ("bytes_left", ctypes.c_uint)]
 
-    lib = snappy_amd.lib()
+    lib = snappy_amd.compat_lib()
     b = Buffer()
     lib.init_Buffer(ctypes.byref(b), 100)
     assert b.current == b.beginning and b.current and b.bytes_left == 100

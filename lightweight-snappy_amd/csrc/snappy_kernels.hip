@@ -1446,13 +1446,45 @@ __device__ __forceinline__ void k4_flush(const uint8_t *ob, uint32_t M, uint8_t 
     }
 }
 
-// literal bytes lsrc[0, kl) straight from HBM to output [kop, kop+kl), in
-// HBM and in the ring (later copies read its tail)
-__device__ __forceinline__ void k4_literal_hbm(const uint8_t *lsrc, uint32_t kl, uint32_t kop, uint8_t *ob, uint32_t M,
+// literal bytes lsrc[0, kl) straight from HBM to output [kop, kop+kl): HBM to
+// HBM in destination-aligned dwords (each funnel-shifted out of two aligned
+// source dwords: an aligned dword holding a byte of the literal never crosses
+// a page the literal does not touch), and its last min(kl, ring) bytes into the
+// ring (later copies read only that far back from the ring; further back, HBM)
+__device__ __noinline__ void k4_literal_hbm(const uint8_t *lsrc, uint32_t kl, uint32_t kop, uint8_t *ob, uint32_t M,
                                                uint8_t *dst, uint32_t lane)
 {
+    uint8_t *const d = dst + kop;
+    const uint32_t h0 = (uint32_t)(-(uintptr_t)d & 3);
+    const uint32_t h = h0 < kl ? h0 : kl;  // head bytes up to a 4-aligned destination
+    if (lane < h) d[lane] = lsrc[lane];
+    const uint32_t nd = (kl - h) >> 2;     // body dwords
+    const uint8_t *const s = lsrc + h;
+    const uint32_t sa = (uint32_t)((uintptr_t)s & 3);
+    const uint32_t *const s4 = reinterpret_cast<const uint32_t *>(s - sa);
+    uint32_t *const d4 = reinterpret_cast<uint32_t *>(d + h);
 #pragma unroll 1
-    for (uint32_t b = 0; b < kl; b += 256) {
+    for (uint32_t i = lane; i < nd; i += 256) {
+        uint32_t w[4];
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            const uint32_t j = i + 64 * m;
+            w[m] = 0;
+            if (j < nd) {
+                const uint32_t lo = __builtin_nontemporal_load(s4 + j);
+                w[m] = sa ? __builtin_amdgcn_alignbit(__builtin_nontemporal_load(s4 + j + 1), lo, 8 * sa) : lo;
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < 4; m++)
+            if (i + 64 * m < nd) d4[i + 64 * m] = w[m];
+    }
+    const uint32_t t = h + 4 * nd;  // tail bytes
+    if (t + lane < kl) d[t + lane] = lsrc[t + lane];
+    // the ring: the literal's last min(kl, M + 1) bytes
+    const uint32_t r0 = kl > M + 1 ? kl - (M + 1) : 0;
+#pragma unroll 1
+    for (uint32_t b = r0; b < kl; b += 256) {
         uint8_t v[4];
 #pragma unroll
         for (int m = 0; m < 4; m++) {
@@ -1462,10 +1494,7 @@ __device__ __forceinline__ void k4_literal_hbm(const uint8_t *lsrc, uint32_t kl,
 #pragma unroll
         for (int m = 0; m < 4; m++) {
             const uint32_t jj = b + 64 * m + lane;
-            if (jj < kl) {
-                ob[(kop + jj) & M] = v[m];
-                dst[kop + jj] = v[m];
-            }
+            if (jj < kl) ob[(kop + jj) & M] = v[m];
         }
     }
 }

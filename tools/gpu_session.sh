@@ -63,6 +63,11 @@ for step in "$@"; do
             timeout -k 10 200 python -u tools/k4_stats.py $kind 268435456 $v > "$out/k4s_${v}_$kind.log" 2>&1
             rc=$?; echo "k4s $v rc=$rc"; cat "$out/k4s_${v}_$kind.log"; [ $rc -ne 0 ] && exit $rc
         done ;;
+    k1s:*)  # k1s:<variant>:<chunk>:<rounds per unit> -> K1r round segments (SNAPPY_K1R_STATS + LSTAMPS build), 256 MiB
+        IFS=: read -r _ v chunk rnds <<< "$step"
+        K1R_CHUNK=$chunk K1R_ROUNDS=$rnds timeout -k 10 200 python -u tools/k1r_stamps.py 268435456 "" $v \
+            > "$out/k1s_${v}_$chunk.log" 2>&1
+        rc=$?; echo "k1s $v rc=$rc"; cat "$out/k1s_${v}_$chunk.log"; [ $rc -ne 0 ] && exit $rc ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

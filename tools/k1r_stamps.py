@@ -7,11 +7,12 @@ os.environ["SNAPPY_AMD_LIB"] = os.path.join(ROOT, "lightweight-snappy_amd", "var
 import numpy as np, torch
 import datagen, snappy_amd
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 8 << 20
-chunk = 32768
+chunk = int(os.environ.get("K1R_CHUNK", "32768"))  # 65536: one SINGLE stream (K1r64)
+layout = snappy_amd.SINGLE if chunk == 65536 else snappy_amd.STREAMS
 a = datagen.make("T", n, 1234)
 x = torch.from_numpy(a).cuda()
 c = snappy_amd.Codec(0)
-comp, offs = c.compress_tensor(x, chunk=chunk, layout=snappy_amd.STREAMS)
+comp, offs = c.compress_tensor(x, chunk=chunk, layout=layout)
 torch.cuda.synchronize()
 class Ctx(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("own", ctypes.c_void_p), ("stream", ctypes.c_void_p),

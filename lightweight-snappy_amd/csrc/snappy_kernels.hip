@@ -306,7 +306,7 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
 #endif
 constexpr uint32_t kK2Seg = SNAPPY_K2_SEG;
 constexpr uint32_t kK2Pass = SNAPPY_K2_PASS;
-constexpr uint32_t kK2Per = kK2Pass / 64;
+[[maybe_unused]] constexpr uint32_t kK2Per = kK2Pass / 64;
 static_assert(kK2Pass % 64 == 0 && kK2Seg % kK2Pass == 0, "K2: passes of 64 k tokens dividing a segment");
 
 // Wave-wide inclusive add-scan in DPP (row_shr 1/2/4/8 inside 16-lane rows,
@@ -2323,7 +2323,7 @@ __device__ __forceinline__ void k5_stage(const uint8_t *__restrict__ comp, uint6
 #ifndef SNAPPY_K5_WIN
 #define SNAPPY_K5_WIN 4096
 #endif
-constexpr uint32_t K5_WIN = SNAPPY_K5_WIN;
+[[maybe_unused]] constexpr uint32_t K5_WIN = SNAPPY_K5_WIN;  // (K5c, decode TU)
 
 // the element at image byte q (rem = stream bytes from it to clen): as k5_parse
 __device__ __forceinline__ bool k5_parse_img(const uint32_t *img, uint32_t q, uint64_t rem, uint64_t &size,

@@ -557,3 +557,30 @@ def test_device_index_past_stream_end_fails_cleanly(codec):
         codec.decompress_tensor(comp, bad, a.size, layout=snappy_amd.SINGLE)
     back = codec.decompress_tensor(comp, offs, a.size, layout=snappy_amd.SINGLE)
     assert torch.equal(back, x)
+
+
+@pytest.mark.parametrize("chunk", [17, 4095, 32768, 65535, 65536])
+def test_any_alignment_long_literals_and_short_copies(codec, chunk):
+    """K4's aligned-dword long-literal copy and its pass paths at every stream
+    and output alignment: incompressible data (literals longer than the
+    window) and short-period data (copies whose source lies in the same
+    64-byte pass), decoded from a stream shifted by 0-3 bytes into an output
+    shifted by 0-3 bytes; nothing outside the output may be written."""
+    import torch
+    layout = snappy_amd.SINGLE if chunk == 65536 else snappy_amd.STREAMS
+    n = 3 * 65536 + 1234
+    for kind, seed in (("R", 5), ("K", 7)):
+        a = datagen.make(kind, n, seed, period=3) if kind == "K" else datagen.make(kind, n, seed)
+        comp, offs = codec.compress_tensor(to_dev(a), chunk=chunk, layout=layout)
+        c = comp.cpu().numpy()
+        for s_in in range(4):
+            d = torch.zeros(c.size + 8, dtype=torch.uint8, device="cuda")
+            d[s_in:s_in + c.size] = comp
+            for s_out in range(4):
+                out = torch.full((n + 8,), 0xA5, dtype=torch.uint8, device="cuda")
+                codec._bind_stream()  # torch's stream: the copies above are ordered before the decode
+                codec.decompress_ptr(d.data_ptr() + s_in, offs.data_ptr(), n, chunk, layout, out.data_ptr() + s_out)
+                torch.cuda.synchronize()
+                got = out.cpu().numpy()
+                assert np.array_equal(got[s_out:s_out + n], a), (kind, chunk, s_in, s_out)
+                assert (got[:s_out] == 0xA5).all() and (got[s_out + n:] == 0xA5).all(), (kind, chunk, s_in, s_out)

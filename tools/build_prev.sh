@@ -25,8 +25,8 @@ for f in snappy_kernels.hip snappy_kernels.h snappy_device.hip; do
     esac
 done
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -Iinclude -I$D $*"
-SC="-mllvm -amdgpu-sched-strategy=max-memory-clause -mllvm -amdgpu-use-amdgpu-trackers"
-SD="-mllvm -amdgpu-sched-strategy=max-ilp"
+SC=${SCHED_C-"-mllvm -amdgpu-sched-strategy=max-memory-clause -mllvm -amdgpu-use-amdgpu-trackers"}  # env SCHED_C overrides (A/B)
+SD=${SCHED_D-"-mllvm -amdgpu-sched-strategy=max-ilp"}
 hipcc $FLAGS $SC -DSNAPPY_TU=1 -x hip -c $D/snappy_kernels.hip -o $P/build/kc_$NAME.o
 hipcc $FLAGS $SD -DSNAPPY_TU=2 -x hip -c $D/snappy_kernels.hip -o $P/build/kd_$NAME.o
 hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -Iinclude -I$D -c $D/snappy_device.hip -o $P/build/dev_$NAME.o

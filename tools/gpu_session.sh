@@ -68,6 +68,17 @@ for step in "$@"; do
         K1R_CHUNK=$chunk K1R_ROUNDS=$rnds timeout -k 10 200 python -u tools/k1r_stamps.py 268435456 "" $v \
             > "$out/k1s_${v}_$chunk.log" 2>&1
         rc=$?; echo "k1s $v rc=$rc"; cat "$out/k1s_${v}_$chunk.log"; [ $rc -ne 0 ] && exit $rc ;;
+    io)  # host I/O floor (tools/io_probe.py, no GPU) and the FILE* API with SNAPPY_AMD_IO_TRACE phase times
+        timeout -k 10 200 python -u tools/io_probe.py 4 > "$out/io_probe.log" 2>&1
+        rc=$?; echo "io_probe rc=$rc"; cat "$out/io_probe.log"; [ $rc -ne 0 ] && exit $rc
+        SNAPPY_AMD_IO_TRACE=1 timeout -k 10 300 python -u -c "import json, bench; print(json.dumps(bench.host_file_api(4 << 30)))" \
+            > "$out/file_api.log" 2>&1
+        rc=$?; echo "file_api rc=$rc"; tail -20 "$out/file_api.log"; [ $rc -ne 0 ] && exit $rc ;;
+    pytest:*)  # pytest:<-k expression, "_or_" for " or "> -> the GPU tests it selects
+        expr=${step#pytest:}; expr=${expr//_or_/ or }
+        timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "$expr" \
+            > "$out/pytest_sel.log" 2>&1
+        rc=$?; echo "pytest rc=$rc"; tail -5 "$out/pytest_sel.log"; fatal $rc && exit $rc ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -24,14 +24,14 @@ for f in snappy_kernels.hip snappy_kernels.h snappy_device.hip; do
     *) git show $REV:$P/csrc/$f > $D/$f ;;
     esac
 done
-FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -Iinclude -I$D $*"
+FLAGS="-O3 -std=c++17 -fPIC --offload-arch=${VARCH:-gfx950} -mcode-object-version=5 -Iinclude -I$D $*"
 SC=${SCHED_C-"-mllvm -amdgpu-sched-strategy=max-memory-clause -mllvm -amdgpu-use-amdgpu-trackers"}  # env SCHED_C overrides (A/B)
 SD=${SCHED_D-"-mllvm -amdgpu-sched-strategy=max-ilp"}
 hipcc $FLAGS $SC -DSNAPPY_TU=1 -x hip -c $D/snappy_kernels.hip -o $P/build/kc_$NAME.o
 hipcc $FLAGS $SD -DSNAPPY_TU=2 -x hip -c $D/snappy_kernels.hip -o $P/build/kd_$NAME.o
-hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -Iinclude -I$D -c $D/snappy_device.hip -o $P/build/dev_$NAME.o
+hipcc -O3 -std=c++17 -fPIC --offload-arch=${VARCH:-gfx950} -mcode-object-version=5 -Iinclude -I$D -c $D/snappy_device.hip -o $P/build/dev_$NAME.o
 gcc -O2 -fPIC -std=gnu11 -Iinclude -c $P/csrc/snappy_host.c -o $P/build/host_var.o
-hipcc --offload-arch=gfx950 -shared -fPIC -o $P/variants/libsnappy_amd_$NAME.so $P/build/kc_$NAME.o $P/build/kd_$NAME.o \
+hipcc --offload-arch=${VARCH:-gfx950} -shared -fPIC -o $P/variants/libsnappy_amd_$NAME.so $P/build/kc_$NAME.o $P/build/kd_$NAME.o \
     $P/build/dev_$NAME.o $P/build/host_var.o
 rm -rf $D
 echo "built $NAME ($REV $*)"

@@ -584,3 +584,60 @@ def test_any_alignment_long_literals_and_short_copies(codec, chunk):
                 got = out.cpu().numpy()
                 assert np.array_equal(got[s_out:s_out + n], a), (kind, chunk, s_in, s_out)
                 assert (got[:s_out] == 0xA5).all() and (got[s_out + n:] == 0xA5).all(), (kind, chunk, s_in, s_out)
+
+
+def test_file_api_positions_and_pipes():
+    """The FILE* entry points from arbitrary stream positions and through pipes
+    (src/snappy_compression.h:8, src/snappy_decompression.h:15): compress a
+    pipe into a regular file after a prefix, decode from an offset inside a
+    file into a pipe, and decode from a pipe (the whole-read path); every
+    output must equal the one-shot stream / the input, the FILE* positions
+    must end where stdio leaves them, and the prefix must be untouched."""
+    import ctypes
+    libc = ctypes.CDLL(None)
+    for fn, res, args in (("fopen", ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_char_p]),
+                          ("popen", ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_char_p]),
+                          ("fclose", ctypes.c_int, [ctypes.c_void_p]), ("pclose", ctypes.c_int, [ctypes.c_void_p]),
+                          ("fseek", ctypes.c_int, [ctypes.c_void_p, ctypes.c_long, ctypes.c_int]),
+                          ("ftell", ctypes.c_long, [ctypes.c_void_p]),
+                          ("fwrite", ctypes.c_size_t, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p])):
+        getattr(libc, fn).restype = res
+        getattr(libc, fn).argtypes = args
+    lib = snappy_amd.lib()
+    data = np.concatenate([datagen.make("T", (9 << 20) + 777, 5), datagen.make("R", 3 << 20, 6)]).tobytes()
+    want = oracle.compress(data)
+    prefix = b"PREFIX-" * 1000
+    with tempfile.TemporaryDirectory() as d:
+        src, snp, dec, dec2 = (os.path.join(d, x) for x in ("in", "in.snp", "dec", "dec2"))
+        open(src, "wb").write(data)
+        # compress: a pipe in, a regular file out after a prefix
+        fi = libc.popen(f"cat {src}".encode(), b"r")
+        fo = libc.fopen(snp.encode(), b"wb")
+        assert libc.fwrite(prefix, 1, len(prefix), fo) == len(prefix)
+        lib.snappy_compress(ctypes.c_void_p(fi), ctypes.c_ulonglong(len(data)), ctypes.c_void_p(fo))
+        assert lib.snappy_amd_last_status() == 0
+        assert libc.ftell(fo) == len(prefix) + len(want)
+        libc.pclose(fi)
+        libc.fclose(fo)
+        blob = open(snp, "rb").read()
+        assert blob[:len(prefix)] == prefix and blob[len(prefix):] == want
+        # decompress: from an offset inside the file, into a pipe
+        fi = libc.fopen(snp.encode(), b"rb")
+        assert libc.fseek(fi, len(prefix), 0) == 0
+        fo = libc.popen(f"cat > {dec}".encode(), b"w")
+        assert lib.snappy_decompress(ctypes.c_void_p(fi), ctypes.c_void_p(fo)) == 0
+        assert libc.ftell(fi) == len(blob)
+        libc.fclose(fi)
+        assert libc.pclose(fo) == 0
+        assert open(dec, "rb").read() == data
+        # decompress: a pipe in (read whole), a regular file out after a prefix
+        open(snp + ".raw", "wb").write(want)
+        fi = libc.popen(f"cat {snp}.raw".encode(), b"r")
+        fo = libc.fopen(dec2.encode(), b"wb")
+        assert libc.fwrite(prefix, 1, len(prefix), fo) == len(prefix)
+        assert lib.snappy_decompress(ctypes.c_void_p(fi), ctypes.c_void_p(fo)) == 0
+        assert libc.ftell(fo) == len(prefix) + len(data)
+        libc.pclose(fi)
+        libc.fclose(fo)
+        out = open(dec2, "rb").read()
+        assert out[:len(prefix)] == prefix and out[len(prefix):] == data

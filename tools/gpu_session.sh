@@ -79,6 +79,11 @@ for step in "$@"; do
         timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "$expr" \
             > "$out/pytest_sel.log" 2>&1
         rc=$?; echo "pytest rc=$rc"; tail -5 "$out/pytest_sel.log"; fatal $rc && exit $rc ;;
+    testsv:*)  # testsv:<variant> -> the GPU tests against variants/libsnappy_amd_<variant>.so (the CLI keeps the main library)
+        v=${step#testsv:}
+        SNAPPY_AMD_LIB=$PWD/lightweight-snappy_amd/variants/libsnappy_amd_$v.so timeout -k 10 700 \
+            python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > "$out/gpu_tests_$v.log" 2>&1
+        rc=$?; echo "testsv $v rc=$rc"; tail -3 "$out/gpu_tests_$v.log"; fatal $rc && exit $rc ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -1873,11 +1873,12 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
         // copy byte whose source lies in the same pass waits for the sub-pass
         // that wrote it (out[op+j] = out[op-off + j mod off], :273-280).
         if (nexec && !(longm && (longm & 1))) {
-            // the ring must hold [F, op_end) and the bitmap the batch's output:
-            // cut the batch (never below one element: the first is <= 508 bytes)
-            const uint64_t over = __ballot(lane < nexec && lane > 0 &&
-                                           ((ring < want && op + out_off + e_len - F > ring - 64) ||
-                                            out_off + e_len > kK4MapBits));
+            // the bitmap must hold the batch's output: cut the batch (never below
+            // one element: the first is <= 508 bytes).  The ring then holds [F,
+            // op_end) too: a batch starts with op - F < 2048 (the flush below),
+            // and 2048 + kK4MapBits <= ring - 64
+            static_assert(2048 + kK4MapBits <= kK4Ring - 64, "K4: the ring must hold [F, op_end)");
+            const uint64_t over = __ballot(lane < nexec && lane > 0 && out_off + e_len > kK4MapBits);
             if (over) nexec = (uint32_t)__builtin_ctzll(over);
             if constexpr (BACK) {
                 // copies reading earlier units: wait until those bytes are in HBM

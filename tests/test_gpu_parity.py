@@ -641,3 +641,21 @@ def test_file_api_positions_and_pipes():
         libc.fclose(fo)
         out = open(dec2, "rb").read()
         assert out[:len(prefix)] == prefix and out[len(prefix):] == data
+
+
+def test_foreign_streams_many_seeds(codec):
+    """Twenty more seeded foreign streams (1-3 MiB: literals of every header
+    width, copies of every kind and distance, overlapping and in-pass copies,
+    elements straddling blocks), decoded by the block-parallel path and by the
+    drop-in host API, against the oracle decoder."""
+    import torch
+    for seed in range(401, 421):
+        n_out = (1 << 20) + (seed * 104729) % (2 << 20)
+        stream = build_stream(random_ops(seed, n_out, [64, 2048, 65535, 1 << 20][seed % 4], max_lit=[70, 700, 70000][seed % 3]))
+        want = oracle.decompress(stream)
+        assert len(want) == n_out
+        d = torch.from_numpy(np.frombuffer(stream, dtype=np.uint8).copy()).cuda()
+        n, offs = codec.index_tensor(d)
+        back = codec.decompress_tensor(d, offs, n, layout=snappy_amd.SINGLE)
+        assert back.cpu().numpy().tobytes() == want, seed
+        assert snappy_amd.decompress(stream) == want, seed

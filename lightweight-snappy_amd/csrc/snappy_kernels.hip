@@ -1868,10 +1868,10 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             }
         }
         // ---- byte passes over the batch output [op, op_end), 64 bytes each:
-        // byte lane l finds its element from the bitmap of element starts in
-        // the pass, literals read the register window, copies read LDS.  A
-        // copy byte whose source lies in the same pass waits for the sub-pass
-        // that wrote it (out[op+j] = out[op-off + j mod off], :273-280).
+        // byte lane l finds its element from the bitmap of element starts,
+        // literals read the window, copies the LDS ring (or HBM beyond it); a
+        // copy byte whose source lies in the same pass takes it from that lane
+        // by pointer jumping (out[op+j] = out[op-off + j mod off], :273-280).
         if (nexec && !(longm && (longm & 1))) {
             // the bitmap must hold the batch's output: cut the batch (never below
             // one element: the first is <= 508 bytes).  The ring then holds [F,

@@ -24,8 +24,8 @@ far = (st[:, 1] >> 32).astype(np.float64)
 st = st.astype(np.float64)
 st[:, 1] = (buf.reshape(units, 8)[:, 1] & 0xFFFFFFFF).astype(np.float64)
 m = st.mean(axis=0)
-print(f"{kind} units {units}: elements/unit {m[1]:.0f} batches {m[2]:.0f} passes {m[3]:.0f} subpasses {m[4]:.0f}"
-      f" sub-passes reading HBM (copies beyond the ring) {far.mean():.0f}")
+print(f"{kind} units {units}: elements/unit {m[1]:.0f} batches {m[2]:.0f} passes {m[3]:.0f} pass steps {m[4]:.0f} (passes + pointer-jump steps)"
+      f" passes reading HBM (copies beyond the ring) {far.mean():.0f}")
 print(f"cycles/unit {m[0]:.0f}  cycles/element {m[0]/m[1]:.1f}  cycles/batch {m[0]/m[2]:.0f}")
 for i, nm in ((5, "window+candidate parse"), (6, "doubling+gather+scans+validate"), (7, "execute (passes)")):
     print(f"  {nm:32s} {m[i]/m[2]:7.0f} cycles/batch  {100*m[i]/m[0]:5.1f}%")

@@ -32,6 +32,8 @@ def orc():
         l.oracle_decompress.argtypes = [vp, sz, vp, sz, ctypes.POINTER(sz)]
         l.oracle_compress_streams.restype = sz
         l.oracle_compress_streams.argtypes = [vp, sz, ctypes.c_uint32, vp, vp, ctypes.c_int]
+        l.oracle_compress_threaded.restype = sz
+        l.oracle_compress_threaded.argtypes = [vp, sz, vp, ctypes.c_int]
         l.oracle_compress_streams_strided.restype = None
         l.oracle_compress_streams_strided.argtypes = [vp, sz, ctypes.c_uint32, vp, sz, vp, ctypes.c_int]
         l.oracle_decompress_streams.restype = ctypes.c_int
@@ -57,6 +59,15 @@ def compress(data) -> bytes:
     out = np.empty(orc().oracle_max_compressed_length(a.size) + 16, dtype=np.uint8)
     n = orc().oracle_compress(_ptr(a), a.size, _ptr(out))
     return out[:n].tobytes()
+
+
+def compress_parallel(a: np.ndarray, threads: int = 16) -> np.ndarray:
+    """compress() of one whole stream with its 65,536-byte blocks spread over
+    `threads` threads (blocks are independent); same bytes, as an array."""
+    a = _arr(a)
+    out = np.empty(orc().oracle_max_compressed_length(a.size) + 16, dtype=np.uint8)
+    n = orc().oracle_compress_threaded(_ptr(a), a.size, _ptr(out), threads)
+    return out[:n]
 
 
 def decompress(data, cap: int | None = None) -> bytes:

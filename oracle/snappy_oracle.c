@@ -325,6 +325,41 @@ size_t oracle_compress_streams(const uint8_t *in, size_t n, uint32_t chunk, uint
     return o;
 }
 
+/* One whole stream (oracle_compress) with its blocks compressed by `nthreads`
+ * threads: snappy_compress() resets the table for every block
+ * (src/snappy_compression.c:419-425), so block b's output depends on block b's
+ * bytes alone and the stream is varint(n) ++ the blocks in order.  Used to
+ * check multi-GiB GPU streams bit for bit. */
+static void *orc_block_worker(void *arg)
+{
+    orc_job *j = (orc_job *)arg;
+    for (size_t s = j->first; s < j->last; s++) {
+        size_t b = s * ORC_MAX_BLOCK;
+        uint32_t L = (uint32_t)((j->n - b) < ORC_MAX_BLOCK ? (j->n - b) : ORC_MAX_BLOCK);
+        j->sizes[s] = oracle_compress_block(j->in + b, L, j->scratch + s * j->stride);
+    }
+    return NULL;
+}
+
+size_t oracle_compress_threaded(const uint8_t *in, size_t n, uint8_t *out, int nthreads)
+{
+    if (n == 0) return 0;
+    size_t nb = (n + ORC_MAX_BLOCK - 1) / ORC_MAX_BLOCK;
+    size_t stride = oracle_max_block_bytes(ORC_MAX_BLOCK) + 16;
+    uint8_t *scratch = (uint8_t *)malloc(nb * stride + 1);
+    size_t *sizes = (size_t *)malloc(nb * sizeof(size_t));
+    orc_job job = {0};
+    job.in = in; job.n = n; job.scratch = scratch; job.stride = stride; job.sizes = sizes;
+    orc_run(&job, nb, nthreads, orc_block_worker);
+    size_t o = oracle_varint_encode(n, out);
+    for (size_t s = 0; s < nb; s++) {
+        memcpy(out + o, scratch + s * stride, sizes[s]);
+        o += sizes[s];
+    }
+    free(scratch); free(sizes);
+    return o;
+}
+
 /* Variant that leaves streams in place at a fixed stride (no compaction);
  * used by the timed CPU baseline so the measurement is the codec only. */
 void oracle_compress_streams_strided(const uint8_t *in, size_t n, uint32_t chunk, uint8_t *scratch,

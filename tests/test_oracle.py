@@ -118,3 +118,30 @@ def test_oracle_decoder_matches_reference_on_foreign_streams():
         stream = build_stream(random_ops(seed, 150_000 + 37_000 * (seed % 5), 131072))
         n = len(oracle.decompress(stream))
         assert oracle.decompress(stream) == oracle.ref_decompress(stream, n)
+
+
+def test_parallel_stream_equals_serial(golden):
+    """compress_parallel (blocks on threads: the checker of the multi-GiB GPU
+    streams) gives the reference's bytes on every golden entry, and compress()'s on
+    multi-block text, random and repeat inputs with ragged ends."""
+    for e in golden["entries"]:  # the reference's own outputs
+        data = np.frombuffer(make_input(e["spec"]), np.uint8).copy()
+        assert sha(oracle.compress_parallel(data, threads=4).tobytes()) == e["out_sha256"], e["name"]
+    for kind, n in (("T", (5 << 20) + 12345), ("R", 3 << 20), ("P", (2 << 20) + 1), ("T", 65536), ("T", 1)):
+        a = datagen.make(kind, n, 7)
+        assert oracle.compress_parallel(a, threads=8).tobytes() == oracle.compress(a.tobytes()), (kind, n)
+    assert oracle.compress_parallel(np.empty(0, np.uint8)).size == 0
+
+
+DIGEST_T1234_5G = "4217993e6c71c372"  # bytes [5 GiB, 5 GiB + 3 MiB) of T seed 1234 (bench.py's text)
+DIGEST_T4321 = "6a90134750bb6f50"  # the first 2 MiB of T seed 4321 (decode10g's tile)
+
+
+def test_datagen_text_known_digests():
+    """The text generator is pinned: bench inputs on the GPU box (and every
+    measurement in profiles/) are these bytes."""
+    a = np.empty(3 << 20, dtype=np.uint8)
+    datagen.fill(a, "T", 1234, offset=5 << 30, threads=4)
+    b = datagen.make("T", 2 << 20, 4321)
+    assert hashlib.sha256(a.tobytes()).hexdigest()[:16] == DIGEST_T1234_5G
+    assert hashlib.sha256(b.tobytes()).hexdigest()[:16] == DIGEST_T4321

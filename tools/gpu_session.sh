@@ -8,6 +8,7 @@ set -o pipefail
 export TMPDIR=/tmp
 out=${1:?outdir}; shift
 mkdir -p "$out"
+export SNAPPY_TEST_PROGRESS=$(cd "$out" && pwd)/test_progress.log
 fatal() { case $1 in 0|1) return 1;; *) return 0;; esac; }
 for step in "$@"; do
     echo "[$(date +%T)] $step"

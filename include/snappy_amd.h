@@ -90,7 +90,8 @@ typedef struct snappy_amd_ctx snappy_amd_ctx;
 
 int snappy_amd_create(int device, snappy_amd_ctx **ctx);
 void snappy_amd_destroy(snappy_amd_ctx *ctx);
-/* Launch on this hipStream_t (NULL = the context's own stream). */
+/* Launch on this hipStream_t (NULL = the context's own stream, a blocking
+ * stream: ordered after work queued on the legacy default stream). */
 int snappy_amd_set_stream(snappy_amd_ctx *ctx, void *hip_stream);
 void *snappy_amd_get_stream(snappy_amd_ctx *ctx);
 

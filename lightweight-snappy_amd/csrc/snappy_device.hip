@@ -83,7 +83,10 @@ int snappy_amd_create(int device, snappy_amd_ctx **out)
     HIP_OK(hipSetDevice(device));
     snappy_amd_ctx *c = new snappy_amd_ctx();
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return SNAPPY_AMD_ERR_DEVICE; }
+    // a blocking stream: work a caller queued on the legacy default stream (torch's
+    // default stream, cuda_stream == 0, which set_stream(NULL) maps here) is
+    // ordered before the context's launches (a non-blocking own stream raced it)
+    if (hipStreamCreateWithFlags(&c->own, hipStreamDefault) != hipSuccess) { delete c; return SNAPPY_AMD_ERR_DEVICE; }
     c->stream = c->own;
     if (hipMalloc(&c->total, 64) != hipSuccess || hipMalloc(&c->k5res, 64) != hipSuccess ||
         hipHostMalloc(&c->h_total, 64, hipHostMallocDefault) != hipSuccess) {

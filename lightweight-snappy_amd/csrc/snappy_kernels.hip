@@ -583,8 +583,15 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     // ---- position window at q0 (see the header): dv = dwords q0/4 .. q0/4 + 63,
     // rotated: dword q0/4 + i sits at lane (dr + i) % 64 (ds_bpermute wraps addr[7:2])
     uint32_t q0 = 0, d0 = 0, dr = 0, dv = 0, bv = 0, hv = 0;
-    uint32_t pdl1 = 0, pdc = 0, ent = 0;      // lane-space data: predecessor lane + 1, its position, entry
-    uint32_t ent_t = 0;                       // the entry's tag (bits 0..7; split table: its own load)
+    uint32_t pdl1 = 0, pdc = 0;               // lane-space data: predecessor lane + 1, its position
+#ifdef SNAPPY_K1R_PACKED3
+    uint32_t ent = 0, ent_t = 0;              // the slot's entry and its tag
+#else
+    // the slot's entry and its tag as the loads' own types: a widened copy would
+    // make the compiler zero-extend (and wait for) a load where it is issued
+    uint16_t ent = 0;
+    uint8_t ent_t = 0;
+#endif
     uint32_t adr = 0, word = 0;               // the lane's table record address and its insert word
     uint32_t pdnz = 0;
     uint64_t m_win = 0, m_win17 = 0;
@@ -726,8 +733,13 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 refresh();
                 lane0 = 1;
             }
-            // the round's table entries: read once per round, at its end, after every
-            // insert of the round (one definition, so no register copy waits for it)
+            // the round's table entries: read right after the round's inserts, so the
+            // read is in flight during the verification (each path that writes the table
+            // again, and a refresh, reads again); the entry registers have the loads' own
+            // u16 / u8 types, or the compiler zero-extends -- and waits for -- each load
+            // where it is issued (round 3: that wait made this order 8 % slower; now
+            // text32k 16.19 -> 16.18 ms, 64 KiB blocks 19.37 -> 19.20, profiles/r03s2b_*;
+            // SNAPPY_K1R_LATE_ENT reads at the round's end instead)
             TBL_READ_ENT(adr);
             for (;;) {
                 LSTAMP(s0);
@@ -769,6 +781,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     const uint32_t lo0 = f > lane0 ? lane0 - 1 : lane0;
                     TBL_INSERT(lane - lo0 <= f - lo0);
                     LDS_ORDER();
+#ifndef SNAPPY_K1R_LATE_ENT
+                    TBL_READ_ENT(adr);  // the next round's entries, in flight during the verification
+#endif
                     LSTAMP(s2);
                     LSEG(1, s1, s2);
                     const uint32_t pv = funnel_bytes(pa, wave_shl1(pa), perm_sel(pf & 3));
@@ -802,6 +817,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                         if (f == lane0) {  // its p - 1, then p again (the later write wins)
                             TBL_INSERT(lane - (lane0 - 1) <= 1);
                             LDS_ORDER();
+#ifndef SNAPPY_K1R_LATE_ENT
+                            TBL_READ_ENT(adr);
+#endif
                         }
                         np = pf + ((skip + f - lane0) >> 5);
                         skip += f - lane0 + 1;
@@ -813,6 +831,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     // update_hash_table :303-307: p_k - 1 and p_k of every miss, lane order
                     TBL_INSERT(lane - (lane0 - 1) <= nk);
                     LDS_ORDER();
+#ifndef SNAPPY_K1R_LATE_ENT
+                    TBL_READ_ENT(adr);
+#endif
                     np = q0 + lane0 + nk - 1 + ((skip + nk - 1) >> 5);  // the last probe steps by 2 at skip 64
                     skip += nk;
 #ifdef SNAPPY_K1R_STATS
@@ -832,8 +853,13 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 if (__builtin_expect(lane0 + SNAPPY_K1R_RMIN > 62, 0)) {
                     refresh();
                     lane0 = 1;
+#ifndef SNAPPY_K1R_LATE_ENT
+                    TBL_READ_ENT(adr);
+#endif
                 }
+#ifdef SNAPPY_K1R_LATE_ENT
                 TBL_READ_ENT(adr);  // every lane (reading only the probe lanes' measured 2.6 % slower)
+#endif
             }
             drain_token();
 #ifdef SNAPPY_K1R_STATS

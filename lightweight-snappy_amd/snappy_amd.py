@@ -362,6 +362,8 @@ class Codec:
 
     # torch-tensor forms ----------------------------------------------------
     def _bind_stream(self):
+        # torch's default stream is the legacy null stream (cuda_stream 0): set_stream(0)
+        # selects the context's own stream, a blocking one, so it is ordered after it too
         self.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
 
     def compress_tensor(self, x, chunk: int = BLOCK, layout: int = SINGLE):

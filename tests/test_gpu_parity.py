@@ -231,6 +231,25 @@ def test_config3_64gib_full_stream(codec):
     torch.cuda.empty_cache()
 
 
+def test_default_stream_ordering(codec):
+    """A tensor written on torch's default stream (the legacy null stream, which
+    the binding maps to the context's own stream) is compressed only after that
+    write: a long spin kernel, then the copy, then compress_tensor at once.
+    (With a non-blocking own stream the compress raced the copy: round 3's
+    decode10g test compressed half-written input.)"""
+    import torch
+    assert torch.cuda.current_stream().cuda_stream == 0
+    a = datagen.make("T", 64 << 20, 99)
+    src = to_dev(a)
+    x = torch.zeros_like(src)
+    torch.cuda.synchronize()
+    torch.cuda._sleep(200_000_000)  # ~0.1 s on the default stream
+    x.copy_(src)
+    comp, offs = codec.compress_tensor(x, chunk=32768, layout=snappy_amd.STREAMS)
+    want, _ = oracle.compress_streams(a, 32768, threads=16)
+    assert np.array_equal(comp.cpu().numpy(), want)
+
+
 @pytest.mark.parametrize("kind,seed", [("R", 1), ("P", 2)])
 def test_full_size_extremes_1gib(codec, kind, seed):
     """configs[2]: 1 GiB random (all-literal) and 64-byte repeat (all-copy),
@@ -471,7 +490,7 @@ def test_decode10g_full_size(codec):
     out = torch.empty(sum(codec.max_output(min(piece, n - o), B, snappy_amd.SINGLE) for o in range(0, n, piece)),
                       dtype=torch.uint8, device="cuda")
     codec._bind_stream()
-    idx, pos = [], 0
+    idx, pos, clens = [], 0, []
     for o in range(0, n, piece):
         m = min(piece, n - o)
         offs = torch.empty(m // B + 2, dtype=torch.int64, device="cuda")
@@ -479,8 +498,9 @@ def test_decode10g_full_size(codec):
                                      n, out.data_ptr() + pos, offs.data_ptr())
         idx.append(offs[:(m + B - 1) // B] + pos)
         pos += clen
+        clens.append(clen)
     idx = torch.cat(idx + [torch.tensor([pos], dtype=torch.int64, device="cuda")])
-    assert pos >= 10_000_000_000 and idx.numel() == n // B + 1
+    assert pos >= 10_000_000_000 and idx.numel() == n // B + 1, (clens, float(x[:GiB].float().mean()))
     back = torch.empty(n, dtype=torch.uint8, device="cuda")
     codec.decompress_ptr(out.data_ptr(), idx.data_ptr(), n, B, snappy_amd.SINGLE, back.data_ptr())
     assert torch.equal(back, x)

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <fcntl.h>
 #include <mutex>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <thread>
 #include <time.h>
@@ -558,15 +559,57 @@ size_t par_io(int fd, uint8_t *buf, size_t len, uint64_t off, bool wr)
     return tot;
 }
 
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23  // Linux 5.14
+#endif
+// memcpy of len bytes into a shared file mapping, split over io_threads()
+// threads in 1 MiB aligned parts; each thread first maps its part's pages
+// writable in one call (MADV_POPULATE_WRITE; on older kernels the copy
+// faults them in)
+void par_copy(uint8_t *dst, const uint8_t *src, size_t len)
+{
+    const int nt = len >= ((size_t)4 << 20) ? io_threads() : 1;
+    const size_t per = ((len / nt) + (1 << 20) - 1) & ~(((size_t)1 << 20) - 1);
+    const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
+    auto part = [&](int t) {
+        const size_t a = std::min(len, per * t), b = std::min(len, per * (t + 1));
+        if (b <= a) return;
+        const uintptr_t lo = (uintptr_t)(dst + a) & ~(pg - 1), hi = (uintptr_t)(dst + b);
+        (void)madvise((void *)lo, hi - lo, MADV_POPULATE_WRITE);
+        memcpy(dst + a, src + a, b - a);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; t++) th.emplace_back(part, t);
+    part(0);
+    for (auto &x : th) x.join();
+}
+
 // A FILE* used from its current position: positional multi-threaded I/O on a
 // regular file (the stdio buffer is flushed / skipped; finish() leaves the
 // FILE* where the stdio calls would have), plain fread / fwrite otherwise
 // (pipes, terminals, files opened for append).
+//
+// A positional writer that knows a bound on what it will write can map the
+// file instead (map_out): the output is then copied into the file's pages by
+// io_threads() threads.  write() / pwrite() of one file serialise on its inode
+// lock (one writer moved 5.9-10.5 GB/s into the GPU box's tmpfs, 8 were
+// slower), faults on distinct pages of a shared mapping do not.  The file is
+// extended to the bound while mapped and cut back to max(its old size, the
+// bytes written) by finish() (or by the destructor on an error path);
+// SNAPPY_AMD_NO_MMAP=1 keeps pwrite().
 struct IoFile {
     FILE *f = nullptr;
     int fd = -1;
     bool pos_io = false;
     uint64_t pos = 0;
+    uint8_t *map = nullptr;
+    size_t map_len = 0;
+    uint64_t map_at = 0, map_end = 0, old_size = 0;
+    int map_fd = -1;
+    IoFile() = default;
+    IoFile(const IoFile &) = delete;
+    IoFile &operator=(const IoFile &) = delete;
+    ~IoFile() { unmap(); }
     bool open(FILE *file, bool wr)
     {
         f = file;
@@ -585,6 +628,54 @@ struct IoFile {
         if (!pos_io || fstat(fd, &st) != 0) return 0;
         return (uint64_t)st.st_size > pos ? (uint64_t)st.st_size - pos : 0;
     }
+    // map [pos, pos + bound) for writing; false (nothing changed) if this file
+    // cannot be mapped: the caller keeps pwrite()
+    bool map_out(uint64_t bound)
+    {
+        if (!pos_io || map || bound < ((uint64_t)64 << 20) || getenv("SNAPPY_AMD_NO_MMAP")) return false;
+        int rfd = fd;
+        if ((fcntl(fd, F_GETFL) & O_ACCMODE) != O_RDWR) {  // a shared mapping needs a read-write descriptor
+            char path[64];
+            snprintf(path, sizeof path, "/proc/self/fd/%d", fd);
+            rfd = ::open(path, O_RDWR | O_CLOEXEC);
+            if (rfd < 0) return false;
+        }
+        struct stat st;
+        const uint64_t end = pos + bound;
+        const long pg = sysconf(_SC_PAGESIZE);
+        bool ok = fstat(rfd, &st) == 0 && S_ISREG(st.st_mode) && pg > 0;
+        if (ok) {
+            old_size = (uint64_t)st.st_size;
+            ok = old_size >= end || ftruncate(rfd, (off_t)end) == 0;
+        }
+        void *m = MAP_FAILED;
+        if (ok) {
+            map_at = pos & ~(uint64_t)(pg - 1);
+            map_len = (size_t)(end - map_at);
+            m = mmap(nullptr, map_len, PROT_READ | PROT_WRITE, MAP_SHARED, rfd, (off_t)map_at);
+        }
+        if (m == MAP_FAILED) {
+            if (ok && old_size < end) (void)ftruncate(rfd, (off_t)old_size);
+            if (rfd != fd) ::close(rfd);
+            return false;
+        }
+        map = static_cast<uint8_t *>(m);
+        map_fd = rfd;
+        map_end = end;
+        return true;
+    }
+    // unmap; the file keeps max(its old size, the bytes written)
+    bool unmap()
+    {
+        if (!map) return true;
+        bool ok = munmap(map, map_len) == 0;
+        const uint64_t keep = std::max(old_size, pos);
+        if (map_end > keep) ok = ftruncate(map_fd, (off_t)keep) == 0 && ok;
+        if (map_fd != fd) ::close(map_fd);
+        map = nullptr;
+        map_fd = -1;
+        return ok;
+    }
     size_t read(uint8_t *b, size_t cap)
     {
         if (!pos_io) return read_full(f, b, cap);
@@ -595,13 +686,19 @@ struct IoFile {
     bool write(const uint8_t *b, size_t len)
     {
         if (!len) return true;
+        if (map) {
+            if (pos + len > map_end) return false;
+            par_copy(map + (pos - map_at), b, len);
+            pos += len;
+            return true;
+        }
         if (!pos_io) return fwrite(b, 1, len, f) == len;
         const size_t put = par_io(fd, const_cast<uint8_t *>(b), len, pos, true);
         pos += put;
         return put == len;
     }
     bool error() const { return !pos_io && ferror(f); }
-    bool finish() { return !pos_io || fseeko(f, (off_t)pos, SEEK_SET) == 0; }
+    bool finish() { return unmap() && (!pos_io || fseeko(f, (off_t)pos, SEEK_SET) == 0); }
 };
 
 void slot_free(StreamSlot &s)
@@ -672,6 +769,9 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
     if (const char *e = getenv("SNAPPY_AMD_DEVICE")) dev = atoi(e);
     IoFile in, out;
     if (!in.open(fin, false) || !out.open(fout, true)) return SNAPPY_AMD_ERR_IO;
+    // (the output stays on pwrite: mapping it, its fresh pages were allocated by
+    // 8 faulting threads, 0.59 -> 0.77 s of writes for 2.3 GB on the GPU box's tmpfs)
+    const bool out_mapped = false;
     int rc;
     for (auto &s : g_slots) {
         if ((rc = slot_init(s, dev))) return rc;
@@ -715,9 +815,9 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
     if (!in.finish() || !out.finish()) return SNAPPY_AMD_ERR_IO;
     if (io_trace())
         fprintf(stderr, "[snappy_amd io] compress %llu -> %llu B: %.3f s (reads %.3f, drain+writes %.3f), %d/%d threads, "
-                        "positional in %d out %d\n",
+                        "positional in %d out %d mapped %d\n",
                 (unsigned long long)total_in, (unsigned long long)base, io_now() - t0, t_rd, t_dr, io_threads(),
-                io_wthreads(), (int)in.pos_io, (int)out.pos_io);
+                io_wthreads(), (int)in.pos_io, (int)out.pos_io, (int)out_mapped);
     if (fidx) {
         // the stream's preamble says header_value; an index is only valid for a
         // stream whose preamble is the length actually compressed
@@ -842,6 +942,7 @@ int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count
     const double t0 = io_now();
     double t_rd = 0;
     uint64_t N = 0;
+    bool out_mapped = false;
     const uint64_t nch = (n + kStreamChunk - 1) / kStreamChunk;
     for (uint64_t k = 0; k < nch; k++) {
         const int s = (int)(k % 3);
@@ -852,10 +953,13 @@ int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count
         t_rd += io_now() - tr;
         if (k == 0) {
             if (snappy_varint_decode(g_dec.h[0], m, &N) == 0) return SNAPPY_AMD_ERR_HEADER;
-            if (out.pos_io && N)
+            if (out.pos_io && N) {
+                // map first: its ftruncate would wait for the whole fallocate (both take the inode lock)
+                out_mapped = out.map_out(N);
                 prealloc = std::thread([fd = out.fd, at = out.pos, N] {
                     (void)fallocate(fd, FALLOC_FL_KEEP_SIZE, (off_t)at, (off_t)N);
                 });
+            }
         }
         HIP_OK(hipMemcpyAsync(c->d_a + k * kStreamChunk, g_dec.h[s], m, hipMemcpyHostToDevice, c->stream));
         HIP_OK(hipEventRecord(g_dec.ev[s], c->stream));
@@ -884,7 +988,9 @@ int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count
     // chunk copied down while this one is written
     const double t2 = io_now();
     double t_wr = 0;
-    if (prealloc.joinable()) prealloc.join();
+    // the mapped writers need not wait for the preallocation: a page it has not
+    // reached yet is allocated by the writer's populate (the preallocation skips it)
+    if (!out_mapped && prealloc.joinable()) prealloc.join();
     const double t3 = io_now();
     const uint64_t och = (N + kStreamChunk - 1) / kStreamChunk;
     auto down = [&](uint64_t k) -> int {
@@ -905,9 +1011,9 @@ int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count
     const bool fin_ok = out.finish();
     if (io_trace())
         fprintf(stderr, "[snappy_amd io] decompress %llu -> %llu B: in %.3f s (reads %.3f), index+decode %.3f s, "
-                        "preallocation wait %.3f s, out %.3f s (writes %.3f), %d/%d threads, positional out %d\n",
+                        "preallocation wait %.3f s, out %.3f s (writes %.3f), %d/%d threads, positional out %d mapped %d\n",
                 (unsigned long long)n, (unsigned long long)N, t1 - t0, t_rd, t2 - t1, t3 - t2, io_now() - t3, t_wr,
-                io_threads(), io_wthreads(), (int)out.pos_io);
+                io_threads(), io_wthreads(), (int)out.pos_io, (int)out_mapped);
     return fin_ok ? SNAPPY_AMD_OK : SNAPPY_AMD_ERR_IO;
 }
 

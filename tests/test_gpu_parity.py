@@ -737,3 +737,72 @@ def test_foreign_streams_many_seeds(codec):
         back = codec.decompress_tensor(d, offs, n, layout=snappy_amd.SINGLE)
         assert back.cpu().numpy().tobytes() == want, seed
         assert snappy_amd.decompress(stream) == want, seed
+
+
+def test_file_api_mapped_outputs():
+    """The FILE* writers that map their output file (IoFile::map_out: outputs
+    >= 64 MiB on a regular file): a file opened "wb" (write-only, so the mapping
+    goes through a read-write reopen) after a prefix, and one opened "r+b" whose
+    old content runs past the new output (kept, size unchanged), in both
+    directions; the results, file sizes and final FILE* positions equal those
+    of the pwrite path (SNAPPY_AMD_NO_MMAP=1)."""
+    import ctypes
+    libc = ctypes.CDLL(None)
+    for fn, res, args in (("fopen", ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_char_p]),
+                          ("fclose", ctypes.c_int, [ctypes.c_void_p]),
+                          ("fseek", ctypes.c_int, [ctypes.c_void_p, ctypes.c_long, ctypes.c_int]),
+                          ("ftell", ctypes.c_long, [ctypes.c_void_p]),
+                          ("fwrite", ctypes.c_size_t, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p])):
+        getattr(libc, fn).restype = res
+        getattr(libc, fn).argtypes = args
+    lib = snappy_amd.lib()
+    data = np.concatenate([datagen.make("T", (150 << 20) + 4321, 8), datagen.make("R", 20 << 20, 9)]).tobytes()
+    want = oracle.compress_parallel(np.frombuffer(data, np.uint8).copy()).tobytes()
+    prefix = b"HEAD-" * 999
+    tail = b"OLD-TAIL" * ((len(data) + 12345) // 8)  # longer than any output below
+    results = {}
+    with tempfile.TemporaryDirectory(dir="/dev/shm" if os.path.isdir("/dev/shm") else None) as d:
+        src = os.path.join(d, "in")
+        open(src, "wb").write(data)
+        for mm in ("1", None):
+            if mm:
+                os.environ["SNAPPY_AMD_NO_MMAP"] = mm
+            try:
+                for mode in ("wb", "r+b"):
+                    snp, dec = os.path.join(d, f"c_{mode}"), os.path.join(d, f"d_{mode}")
+                    for path in (snp, dec):
+                        open(path, "wb").write(prefix + (tail if mode == "r+b" else b""))
+                    fi, fo = libc.fopen(src.encode(), b"rb"), libc.fopen(snp.encode(), mode.encode())
+                    if mode == "wb":  # ("wb" truncated the file: the prefix again, through stdio)
+                        assert libc.fwrite(prefix, 1, len(prefix), fo) == len(prefix)
+                    assert libc.fseek(fo, len(prefix), 0) == 0
+                    lib.snappy_compress(ctypes.c_void_p(fi), ctypes.c_ulonglong(len(data)), ctypes.c_void_p(fo))
+                    assert lib.snappy_amd_last_status() == 0
+                    cpos = libc.ftell(fo)
+                    libc.fclose(fi), libc.fclose(fo)
+                    fi, fo = libc.fopen(snp.encode(), b"rb"), libc.fopen(dec.encode(), mode.encode())
+                    if mode == "wb":
+                        assert libc.fwrite(prefix, 1, len(prefix), fo) == len(prefix)
+                    assert libc.fseek(fi, len(prefix), 0) == 0 and libc.fseek(fo, len(prefix), 0) == 0
+                    if mode == "r+b":  # the stream ends before the old tail: decode exactly the stream
+                        open(snp + ".s", "wb").write(want)
+                        libc.fclose(fi)
+                        fi = libc.fopen((snp + ".s").encode(), b"rb")
+                    assert lib.snappy_decompress(ctypes.c_void_p(fi), ctypes.c_void_p(fo)) == 0
+                    dpos = libc.ftell(fo)
+                    libc.fclose(fi), libc.fclose(fo)
+                    cblob, dblob = open(snp, "rb").read(), open(dec, "rb").read()
+                    assert cpos == len(prefix) + len(want) and dpos == len(prefix) + len(data), (mm, mode)
+                    assert cblob[:len(prefix)] == prefix and cblob[len(prefix):cpos] == want, (mm, mode)
+                    assert dblob[:len(prefix)] == prefix and dblob[len(prefix):dpos] == data, (mm, mode)
+                    if mode == "wb":
+                        assert len(cblob) == cpos and len(dblob) == dpos, (mm, mode)
+                    else:  # the old content past the output is untouched, the size unchanged
+                        size = len(prefix) + len(tail)
+                        assert len(cblob) == size and cblob[cpos:] == tail[cpos - len(prefix):], (mm, mode)
+                        assert len(dblob) == size and dblob[dpos:] == tail[dpos - len(prefix):], (mm, mode)
+                    results[(mm, mode)] = (len(cblob), len(dblob), cpos, dpos)
+            finally:
+                os.environ.pop("SNAPPY_AMD_NO_MMAP", None)
+    for mode in ("wb", "r+b"):
+        assert results[("1", mode)] == results[(None, mode)]

@@ -15,10 +15,12 @@ WLS=${*:-"text32k text64k random repeat decode10g"}
 STEPS=${STEPS:-5}
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"
 run() {  # workload
-    local w=$1 d=gpurun_out/prof/$1 q="--workload $1 --no-cpu-baseline --no-host-e2e"
+    # --no-sub: the profiled process runs this workload only (the default line also runs the
+    # other configs, whose launches of the same kernels would be averaged into W's counters)
+    local w=$1 d=gpurun_out/prof/$1 q="--workload $1 --no-cpu-baseline --no-host-e2e --no-sub"
     mkdir -p $d &&
     echo "[$(date +%T)] $w: bench" &&
-    timeout -k 10 400 python3 bench.py --workload $w --steps $STEPS --warmup 2 --cpu-sample-bytes 268435456 \
+    timeout -k 10 400 python3 bench.py --workload $w --steps $STEPS --warmup 2 --cpu-sample-bytes 268435456 --no-sub \
         > $d/bench.json 2> $d/bench.err &&
     echo "[$(date +%T)] $w: kernel trace" &&
     timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $d/trace -o run --output-format csv -- \

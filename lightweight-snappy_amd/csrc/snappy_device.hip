@@ -731,10 +731,39 @@ int slot_init(StreamSlot &s, int device)
     return SNAPPY_AMD_OK;
 }
 
+// The compressed chunks go to the file from a writer thread, one chunk at a
+// time and in order, so writing chunk k-1 overlaps reading chunk k+1 (the two
+// use different buffers of the slot); wait() joins the chunk in flight.
+struct AsyncWriter {
+    std::thread t;
+    bool ok = true;
+    double busy = 0;  // seconds spent writing (SNAPPY_AMD_IO_TRACE)
+    void wait()
+    {
+        if (t.joinable()) t.join();
+    }
+    // false if an earlier chunk failed to write (nothing more is written)
+    bool start(IoFile &f, const uint8_t *b, size_t len)
+    {
+        wait();
+        if (!ok) return false;
+        t = std::thread([this, &f, b, len] {
+            const double t0 = io_now();
+            ok = f.write(b, len);
+            busy += io_now() - t0;
+        });
+        return true;
+    }
+    ~AsyncWriter() { wait(); }
+};
+
 // finish slot s: its compressed size is in s.c->h_total once its stream drains.
 // With a sidecar file, the chunk's block index goes out too, shifted by the
 // stream bytes written before it (*base); the stream-end entry is left to the caller.
-int slot_drain(StreamSlot &s, IoFile &fout, FILE *fidx, uint64_t *base)
+// The chunk's bytes are handed to the writer (the slot's h_out stays in use
+// until the next drain's start() joins it: the slots alternate, so that is
+// two drains before this slot's h_out is filled again).
+int slot_drain(StreamSlot &s, AsyncWriter &wr, IoFile &fout, FILE *fidx, uint64_t *base)
 {
     if (!s.busy) return SNAPPY_AMD_OK;
     s.busy = false;
@@ -744,7 +773,7 @@ int slot_drain(StreamSlot &s, IoFile &fout, FILE *fidx, uint64_t *base)
     HIP_OK(hipMemcpyAsync(s.h_out, s.d_out, len, hipMemcpyDeviceToHost, s.c->stream));
     if (fidx) HIP_OK(hipMemcpyAsync(s.h_idx, s.d_idx, units * sizeof(uint64_t), hipMemcpyDeviceToHost, s.c->stream));
     HIP_OK(hipStreamSynchronize(s.c->stream));
-    if (!fout.write(s.h_out, len)) return SNAPPY_AMD_ERR_IO;
+    if (!wr.start(fout, s.h_out, len)) return SNAPPY_AMD_ERR_IO;
     if (fidx) {
         for (size_t i = 0; i < units; i++) s.h_idx[i] += *base;
         if (fwrite(s.h_idx, sizeof(uint64_t), units, fidx) != units) return SNAPPY_AMD_ERR_IO;
@@ -768,6 +797,7 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
     int dev = 0;
     if (const char *e = getenv("SNAPPY_AMD_DEVICE")) dev = atoi(e);
     IoFile in, out;
+    AsyncWriter wr;  // (declared after out: joined before out is destroyed)
     if (!in.open(fin, false) || !out.open(fout, true)) return SNAPPY_AMD_ERR_IO;
     // (the output stays on pwrite: mapping it, its fresh pages were allocated by
     // 8 faulting threads, 0.59 -> 0.77 s of writes for 2.3 GB on the GPU box's tmpfs)
@@ -801,7 +831,7 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
         // chunk k-1 out while chunk k runs, then chunk k+1 in (its slot is free
         // once chunk k-1 drained)
         const double td = io_now();
-        if ((rc = slot_drain(o, out, fidx, &base))) return rc;
+        if ((rc = slot_drain(o, wr, out, fidx, &base))) return rc;
         const double tr = io_now();
         n = in.read(o.h_in, kStreamChunk);
         t_rd += io_now() - tr;
@@ -810,13 +840,15 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
     }
     // the slots drain in chunk order: the one holding the last chunk goes last
     const uint32_t last = total_in ? (uint32_t)(((total_in + kStreamChunk - 1) / kStreamChunk - 1) & 1) : 0;
-    if ((rc = slot_drain(g_slots[last ^ 1], out, fidx, &base))) return rc;
-    if ((rc = slot_drain(g_slots[last], out, fidx, &base))) return rc;
+    if ((rc = slot_drain(g_slots[last ^ 1], wr, out, fidx, &base))) return rc;
+    if ((rc = slot_drain(g_slots[last], wr, out, fidx, &base))) return rc;
+    wr.wait();
+    if (!wr.ok) return SNAPPY_AMD_ERR_IO;
     if (!in.finish() || !out.finish()) return SNAPPY_AMD_ERR_IO;
     if (io_trace())
-        fprintf(stderr, "[snappy_amd io] compress %llu -> %llu B: %.3f s (reads %.3f, drain+writes %.3f), %d/%d threads, "
+        fprintf(stderr, "[snappy_amd io] compress %llu -> %llu B: %.3f s (reads %.3f, drains %.3f, writes %.3f overlapped), %d/%d threads, "
                         "positional in %d out %d mapped %d\n",
-                (unsigned long long)total_in, (unsigned long long)base, io_now() - t0, t_rd, t_dr, io_threads(),
+                (unsigned long long)total_in, (unsigned long long)base, io_now() - t0, t_rd, t_dr, wr.busy, io_threads(),
                 io_wthreads(), (int)in.pos_io, (int)out.pos_io, (int)out_mapped);
     if (fidx) {
         // the stream's preamble says header_value; an index is only valid for a
@@ -984,8 +1016,8 @@ int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count
     if ((rc = snappy_amd_decompress_device(c, c->d_a, c->d_idx, (size_t)N, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE,
                                            c->d_b)))
         return rc;
-    // (3) HBM -> pinned chunk (copy engine) -> file (host threads), the next
-    // chunk copied down while this one is written
+    // (3) HBM -> pinned chunk (copy engine) -> file (a writer thread, itself
+    // using several threads on a mapped output)
     const double t2 = io_now();
     double t_wr = 0;
     // the mapped writers need not wait for the preallocation: a page it has not
@@ -999,20 +1031,33 @@ int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count
         HIP_OK(hipEventRecord(g_dec.ev[k % 3], c->stream));
         return SNAPPY_AMD_OK;
     };
+    // two chunks copied down ahead of the one being written (by the writer thread:
+    // chunk k's slot is refilled with chunk k + 3 once its write has been joined)
     if ((rc = down(0))) return rc;
+    if (och > 1 && (rc = down(1))) return rc;
+    AsyncWriter wr;  // (after out: joined before out is destroyed)
+    double t_ev = 0, t_join = 0;
     for (uint64_t k = 0; k < och; k++) {
-        if (k + 1 < och && (rc = down(k + 1))) return rc;
+        const double te = io_now();
         HIP_OK(hipEventSynchronize(g_dec.ev[k % 3]));
         const size_t m = (size_t)std::min<uint64_t>(kStreamChunk, N - k * kStreamChunk);
-        const double tw = io_now();
-        if (!out.write(g_dec.h[k % 3], m)) return SNAPPY_AMD_ERR_IO;
-        t_wr += io_now() - tw;
+        const double tj = io_now();
+        t_ev += tj - te;
+        const bool started = wr.start(out, g_dec.h[k % 3], m);  // joins chunk k - 1's write
+        t_join += io_now() - tj;
+        if (!started) return SNAPPY_AMD_ERR_IO;
+        if (k + 2 < och && (rc = down(k + 2))) return rc;                 // into chunk k - 1's slot
     }
+    wr.wait();
+    t_wr = wr.busy;
+    if (!wr.ok) return SNAPPY_AMD_ERR_IO;
     const bool fin_ok = out.finish();
     if (io_trace())
         fprintf(stderr, "[snappy_amd io] decompress %llu -> %llu B: in %.3f s (reads %.3f), index+decode %.3f s, "
-                        "preallocation wait %.3f s, out %.3f s (writes %.3f), %d/%d threads, positional out %d mapped %d\n",
-                (unsigned long long)n, (unsigned long long)N, t1 - t0, t_rd, t2 - t1, t3 - t2, io_now() - t3, t_wr,
+                        "preallocation wait %.3f s, out %.3f s (copy waits %.3f, writer waits %.3f, writes %.3f), "
+                        "%d/%d threads, positional out %d mapped %d\n",
+                (unsigned long long)n, (unsigned long long)N, t1 - t0, t_rd, t2 - t1, t3 - t2, io_now() - t3, t_ev,
+                t_join, t_wr,
                 io_threads(), io_wthreads(), (int)out.pos_io, (int)out_mapped);
     return fin_ok ? SNAPPY_AMD_OK : SNAPPY_AMD_ERR_IO;
 }

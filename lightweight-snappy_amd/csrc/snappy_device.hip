@@ -604,7 +604,7 @@ struct IoFile {
     uint64_t pos = 0;
     uint8_t *map = nullptr;
     size_t map_len = 0;
-    uint64_t map_at = 0, map_end = 0, old_size = 0;
+    uint64_t map_at = 0, map_end = 0, old_size = 0, map_from = 0;
     int map_fd = -1;
     IoFile() = default;
     IoFile(const IoFile &) = delete;
@@ -662,14 +662,16 @@ struct IoFile {
         map = static_cast<uint8_t *>(m);
         map_fd = rfd;
         map_end = end;
+        map_from = pos;
         return true;
     }
-    // unmap; the file keeps max(its old size, the bytes written)
+    // unmap; the file keeps max(its old size, the end of the bytes written) --
+    // its old size if nothing was written (an error before the first chunk)
     bool unmap()
     {
         if (!map) return true;
         bool ok = munmap(map, map_len) == 0;
-        const uint64_t keep = std::max(old_size, pos);
+        const uint64_t keep = pos > map_from ? std::max(old_size, pos) : old_size;
         if (map_end > keep) ok = ftruncate(map_fd, (off_t)keep) == 0 && ok;
         if (map_fd != fd) ::close(map_fd);
         map = nullptr;

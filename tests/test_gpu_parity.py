@@ -806,3 +806,41 @@ def test_file_api_mapped_outputs():
                 os.environ.pop("SNAPPY_AMD_NO_MMAP", None)
     for mode in ("wb", "r+b"):
         assert results[("1", mode)] == results[(None, mode)]
+
+
+def test_file_api_mapped_output_error_leaves_file():
+    """A FILE* decode that fails after its output was mapped (a 100 MiB header
+    over a corrupt body) leaves the output file as it was: the same size (even
+    with the FILE* positioned past its end, where stdio would not have extended
+    it) and the same bytes; the pwrite path (SNAPPY_AMD_NO_MMAP=1) agrees."""
+    import ctypes
+    libc = ctypes.CDLL(None)
+    for fn, res, args in (("fopen", ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_char_p]),
+                          ("fclose", ctypes.c_int, [ctypes.c_void_p]),
+                          ("fseek", ctypes.c_int, [ctypes.c_void_p, ctypes.c_long, ctypes.c_int])):
+        getattr(libc, fn).restype = res
+        getattr(libc, fn).argtypes = args
+    lib = snappy_amd.lib()
+    n = 100 << 20
+    rng = np.random.default_rng(11)
+    body = bytes([0x01]) + rng.integers(0, 256, 3 << 20, dtype=np.uint8).tobytes()  # copy-1 at output 0: bad offset
+    stream = snappy_amd.varint_encode(n) + body
+    prefix = b"KEEP-ME-" * 512
+    with tempfile.TemporaryDirectory(dir="/dev/shm" if os.path.isdir("/dev/shm") else None) as d:
+        src = os.path.join(d, "bad.snp")
+        open(src, "wb").write(stream)
+        for mm in ("1", None):
+            if mm:
+                os.environ["SNAPPY_AMD_NO_MMAP"] = mm
+            try:
+                for mode, seek in (("r+b", 0), ("r+b", 4096)):
+                    dec = os.path.join(d, f"out_{mm}_{seek}")
+                    open(dec, "wb").write(prefix)
+                    fi, fo = libc.fopen(src.encode(), b"rb"), libc.fopen(dec.encode(), mode.encode())
+                    assert libc.fseek(fo, len(prefix) + seek, 0) == 0
+                    rc = lib.snappy_decompress(ctypes.c_void_p(fi), ctypes.c_void_p(fo))
+                    libc.fclose(fi), libc.fclose(fo)
+                    assert rc != 0, (mm, seek)
+                    assert open(dec, "rb").read() == prefix, (mm, seek)
+            finally:
+                os.environ.pop("SNAPPY_AMD_NO_MMAP", None)

@@ -2001,9 +2001,15 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 // reads garbage, replaced below) and writes (a lane past op_end to the
                 // dummy byte after the ring): no exec changes
                 const bool inpass = pend && !direct && src >= (SrcT)P;
-                const uint32_t rv = ob[(uint32_t)src & M];
-                uint32_t val = lit ? lb : (far ? fv : rv);
-                if (__builtin_expect(__ballot(inpass) != 0, 0)) {
+                // two selects, each over values every lane loaded, kept as bytes: with
+                // val = lit ? lb : (far ? fv : rv) the compiler sank the ring read into an
+                // exec-masked region for the copy lanes and zero-extended (and waited for)
+                // the window byte where it was read (K4 text32k 3.18 -> 3.10 ms per GiB,
+                // 64 KiB blocks 3.45 -> 3.36; profiles/r03s2r_*)
+                const uint8_t rv = ob[(uint32_t)src & M];
+                const uint8_t lr = lit ? (uint8_t)lb : rv;
+                uint32_t val = far ? fv : (uint32_t)lr;
+                                if (__builtin_expect(__ballot(inpass) != 0, 0)) {
                     // out[op+j] = out[op-off + j mod off] (:273-280) with the source in
                     // this pass: lane src - P (a lower lane) holds it.  Follow those
                     // links by pointer jumping to a lane whose value is known (direct,

@@ -26,7 +26,7 @@ for f in snappy_kernels.hip snappy_kernels.h snappy_device.hip; do
 done
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=${VARCH:-gfx950} -mcode-object-version=5 -Iinclude -I$D $*"
 SC=${SCHED_C-"-mllvm -amdgpu-sched-strategy=max-memory-clause -mllvm -amdgpu-use-amdgpu-trackers"}  # env SCHED_C overrides (A/B)
-SD=${SCHED_D-"-mllvm -amdgpu-sched-strategy=max-ilp"}
+SD=${SCHED_D-"-mllvm -amdgpu-sched-strategy=max-ilp -mllvm -amdgpu-use-amdgpu-trackers"}
 hipcc $FLAGS $SC -DSNAPPY_TU=1 -x hip -c $D/snappy_kernels.hip -o $P/build/kc_$NAME.o
 hipcc $FLAGS $SD -DSNAPPY_TU=2 -x hip -c $D/snappy_kernels.hip -o $P/build/kd_$NAME.o
 hipcc -O3 -std=c++17 -fPIC --offload-arch=${VARCH:-gfx950} -mcode-object-version=5 -Iinclude -I$D -c $D/snappy_device.hip -o $P/build/dev_$NAME.o

@@ -273,6 +273,9 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
 #define SNAPPY_K1R_DMAX 10  // lane-space rounds: same-hash distances resolved per window
                             // (8/10/12/14/16 measured; profiles/r03h_ab_k1r_dmax_rmin_*)
 #endif
+#ifndef SNAPPY_K1R_DMAX64
+#define SNAPPY_K1R_DMAX64 SNAPPY_K1R_DMAX  // the same for 65,536-byte blocks (K1r64)
+#endif
 #ifndef SNAPPY_K1R_LSMIN
 #define SNAPPY_K1R_LSMIN 4  // lane-space rounds while at least this many step-1 probes remain
 #endif
@@ -344,7 +347,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                                          uint32_t *__restrict__ seg_off, uint32_t segs)
 {
     constexpr int W = SNAPPY_K1R_WINDOW;
-    constexpr uint32_t DMAX = SNAPPY_K1R_DMAX;
+    constexpr uint32_t DMAX = BIG ? SNAPPY_K1R_DMAX64 : SNAPPY_K1R_DMAX;
     static_assert(SNAPPY_K1R_LSMIN >= 4 && SNAPPY_K1R_LSMIN <= 32, "lane-space rounds need skip < 64 - 3");
     static_assert(DMAX >= 2 && DMAX <= 16, "DMAX: 2..16 (kcap <= 15 keeps the lane masks in range)");
     // 12 KiB: 4096 packed 3-byte records (u16 position, u8 tag) at byte 3 * slot:

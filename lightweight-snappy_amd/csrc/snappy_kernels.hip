@@ -270,17 +270,20 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
 }
 
 #ifndef SNAPPY_K1R_DMAX
-#define SNAPPY_K1R_DMAX 10  // lane-space rounds: same-hash distances resolved per window
-                            // (8/10/12/14/16 measured; profiles/r03h_ab_k1r_dmax_rmin_*)
+#define SNAPPY_K1R_DMAX 9  // lane-space rounds: same-hash distances resolved per window (8/10/12/14/16
+                           // measured, profiles/r03h_ab_k1r_dmax_rmin_*; after the early entry read
+                           // 9 / 10 / 12: 16.07 / 16.19 / 16.18 ms per GiB, profiles/r03s2z_*, r03s2aa_*)
 #endif
 #ifndef SNAPPY_K1R_DMAX64
-#define SNAPPY_K1R_DMAX64 SNAPPY_K1R_DMAX  // the same for 65,536-byte blocks (K1r64)
+#define SNAPPY_K1R_DMAX64 10  // K1r64 (65,536-byte blocks): 9 / 10 / 12 -> 19.29 / 19.23 / 19.32 ms
 #endif
 #ifndef SNAPPY_K1R_LSMIN
 #define SNAPPY_K1R_LSMIN 4  // lane-space rounds while at least this many step-1 probes remain
 #endif
 #ifndef SNAPPY_K1R_RMIN
-#define SNAPPY_K1R_RMIN 8  // refresh the window when fewer probe lanes remain
+#define SNAPPY_K1R_RMIN 6  // refresh the window when fewer probe lanes remain (6 / 8 / 10 after the
+                           // early entry read: 16.14 / 16.19 / 16.26 ms per GiB, 64 KiB blocks
+                           // 19.15 / 19.23 / 19.30; profiles/r03s2z_*)
 #endif
 #ifndef SNAPPY_K1R_WINDOW
 #define SNAPPY_K1R_WINDOW 4  // W-probe rounds

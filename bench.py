@@ -5,20 +5,24 @@ One step = one compress (K1r match finder + K3 scan + K2 emit) and one
 decompress (K4) of the rank's batch, inputs already resident in HBM.
 
 Workloads (BASELINE.json configs):
-  N = 1, default   configs[1]: 1 GiB of synthetic enwik8-like text as 32,768
+  default, any N   configs[3], the metric's own curve ("at 1/2/4/8 MI355X"):
+                   64 GiB of synthetic enwik8-like text as 2,097,152
                    independent 32 KiB streams (each == the reference's
-                   snappy_compress() of its chunk).  The same JSON line then
-                   carries compact sub-results for the other single-GPU
-                   configs -- text64k (one snappy_compress() stream of 64 KiB
-                   blocks), random + repeat (configs[2]), decode10g
-                   (configs[4]) -- and host_file_api, the FILE* entry points
-                   cmd.c calls, on a 4 GiB file in /dev/shm.
-  N > 1, default   configs[3]: 64 GiB of 32 KiB text streams in total,
-                   strong-scaled over the N ranks (rank r owns the
-                   unit-aligned range dist.shard_range(64 GiB, N, r)).
-  --weak           N > 1 with --bytes-per-gpu per rank instead.
-  --total-bytes T  any fixed job size (the N = 1 point of configs[3] is
-                   --gpus 1 --total-bytes 68719476736).
+                   snappy_compress() of its chunk), strong-scaled over the N
+                   ranks (rank r owns the unit-aligned range
+                   dist.shard_range(64 GiB, N, r)), so --gpus 1/2/4/8 is one
+                   job on one curve.  At N = 1 the same JSON line carries
+                   compact sub-results for the other configs -- text32k
+                   (configs[1]: 1 GiB of the same streams), text64k (one
+                   snappy_compress() stream of 64 KiB blocks), random +
+                   repeat (configs[2]), decode10g (configs[4]), config0 (the
+                   1,000,000-byte text file through the FILE* API, the
+                   compiled reference beside it) -- and host_file_api, the
+                   FILE* entry points cmd.c calls, on a 4 GiB file in /dev/shm.
+  --workload W     W alone: 1 GiB per rank at N = 1 (decode10g: its ~10 GB
+                   stream), 64 GiB strong-scaled at N > 1.
+  --weak / --bytes-per-gpu B   B bytes per rank (default 1 GiB).
+  --total-bytes T  any fixed job size, strong-scaled.
 
 Exchange steps: C1, the all-gather of the shard sizes, is part
 of every step.  With N > 1 a second timed loop runs the whole job end to
@@ -78,7 +82,8 @@ WORKLOADS = {
 }
 DECODE_ONLY = {"decode10g"}
 DECODE10G_BYTES = (18_500_000_000 // 65536) * 65536  # ratio ~1.85 -> ~10 GB of compressed stream
-SUB_WORKLOADS = ("text64k", "random", "repeat", "decode10g")
+SUB_WORKLOADS = ("text32k", "text64k", "random", "repeat", "decode10g")
+CONFIG0_BYTES = 1_000_000  # BASELINE configs[0]: one 1 MB text buffer (src/snappy_test.c:7)
 
 
 def parse(argv=None):
@@ -87,11 +92,12 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="text32k", choices=sorted(WORKLOADS))
-    ap.add_argument("--bytes-per-gpu", type=int, default=GiB, help="weak scaling: input bytes per rank")
+    ap.add_argument("--bytes-per-gpu", type=int, default=None,
+                    help="weak scaling: input bytes per rank (default 1 GiB with --weak)")
     ap.add_argument("--total-bytes", type=int, default=0,
-                    help="strong scaling: fixed job size sharded over the ranks (default with N > 1: "
-                         "68719476736 = configs[3])")
-    ap.add_argument("--weak", action="store_true", help="N > 1: --bytes-per-gpu per rank instead of configs[3]")
+                    help="strong scaling: fixed job size sharded over the ranks (default: 68719476736 = "
+                         "configs[3] for text32k at every N and for every workload at N > 1)")
+    ap.add_argument("--weak", action="store_true", help="--bytes-per-gpu per rank instead of configs[3]")
     ap.add_argument("--piece-bytes", type=int, default=8 * GiB,
                     help="a rank compresses its range in pieces of at most this many bytes (bounds token scratch)")
     ap.add_argument("--no-assemble", action="store_true", help="N > 1: skip the end-to-end loop with C2")
@@ -108,16 +114,9 @@ def parse(argv=None):
                     help="nccl (= RCCL, the real path) or gloo (CPU collectives; rehearsal with ranks sharing a GPU)")
     ap.add_argument("--cpu-sample-bytes", type=int, default=GiB)
     ap.add_argument("--pmc", default=None,
-                    help="rocprofv3 PMC summary giving HBM traffic per launch (default profiles/pmc_<workload>.json, "
-                         "written by tools/pmc_summary.py)")
-    a = ap.parse_args(argv)
-    if a.pmc is None:
-        a.pmc = pmc_path(a.workload)
-    return a
-
-
-def pmc_path(workload: str) -> str:
-    return os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+                    help="rocprofv3 PMC summary giving HBM traffic per launch (default: the profiles/pmc_*.json "
+                         "written by tools/pmc_summary.py for this workload and launch size)")
+    return ap.parse_args(argv)
 
 
 def _free_port() -> int:
@@ -311,6 +310,72 @@ def host_file_api(nbytes: int) -> dict:
                     "file I/O + PCIe + kernels"}
 
 
+def config0_file_api(reps: int = 20) -> dict:
+    """BASELINE configs[0] as stated: snappy_compress + snappy_decompress
+    (src/cmd.c:90-98's calls) on one 1,000,000-byte text buffer written to a
+    file in /dev/shm -- the compiled reference (oracle/_ref/libsnappy_ref.so,
+    1 core; CPU-baseline leg only) and libsnappy_amd.so's FILE* path side by
+    side on the same file, in-process through libc stdio, best of `reps`.
+    Both outputs are checked: the two compressed files byte-identical, both
+    decodes equal to the input.  MB/s = input bytes / wall second, as
+    src/result.c:30-31 prints them."""
+    lib = snappy_amd.lib()
+    libc = ctypes.CDLL(None)
+    libc.fopen.restype = ctypes.c_void_p
+    libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    libc.fclose.argtypes = [ctypes.c_void_p]
+    ref_path = os.path.join(ROOT, "oracle", "_ref", "libsnappy_ref.so")
+    ref = ctypes.CDLL(ref_path) if os.path.exists(ref_path) else None  # RTLD_LOCAL: its own snappy_compress
+    a = datagen.make("T", CONFIG0_BYTES, 1234)  # golden entry text_1000000
+    d = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    res = {"workload": "config0: 1,000,000 B of synthetic text (golden text_1000000), one snappy_compress() stream, "
+                       "FILE* API in and out of /dev/shm", "bytes": CONFIG0_BYTES}
+    with tempfile.TemporaryDirectory(dir=d, prefix="snappy_c0_") as tmp:
+        src = os.path.join(tmp, "in").encode()
+        a.tofile(src.decode())
+
+        def time_lib(l, tag):
+            snp, dec = (os.path.join(tmp, f"{tag}.{x}").encode() for x in ("snp", "dec"))
+            best_c = best_d = float("inf")
+            for _ in range(reps):
+                for mode in (0, 1):
+                    fi = libc.fopen(src if mode == 0 else snp, b"rb")
+                    fo = libc.fopen(snp if mode == 0 else dec, b"wb")
+                    assert fi and fo
+                    t0 = time.perf_counter()
+                    if mode == 0:
+                        l.snappy_compress(ctypes.c_void_p(fi), ctypes.c_ulonglong(CONFIG0_BYTES), ctypes.c_void_p(fo))
+                    else:
+                        l.snappy_decompress(ctypes.c_void_p(fi), ctypes.c_void_p(fo))
+                    libc.fclose(ctypes.c_void_p(fo))
+                    t = time.perf_counter() - t0
+                    libc.fclose(ctypes.c_void_p(fi))
+                    if mode == 0:
+                        best_c = min(best_c, t)
+                    else:
+                        best_d = min(best_d, t)
+            comp = open(snp.decode(), "rb").read()
+            ok = open(dec.decode(), "rb").read() == a.tobytes()
+            return {"compress_MBps": round(CONFIG0_BYTES / best_c / 1e6, 1),
+                    "decompress_MBps": round(CONFIG0_BYTES / best_d / 1e6, 1),
+                    "round_trip_MBps": round(CONFIG0_BYTES / (best_c + best_d) / 1e6, 1),
+                    "compressed_bytes": len(comp), "round_trip_ok": ok}, comp
+
+        gpu, comp_gpu = time_lib(lib, "gpu")
+        assert lib.snappy_amd_last_status() == 0
+        res["gpu_file_api"] = dict(gpu, note="libsnappy_amd.so snappy_compress/snappy_decompress, 1 MI355X: one "
+                                             "65,536-byte-block stream, PCIe + launch latency dominate at 1 MB")
+        ok = gpu["round_trip_ok"]
+        if ref is not None:
+            r, comp_ref = time_lib(ref, "ref")
+            res["cpu_reference"] = dict(r, cores=1, kind="reference",
+                                        note=f"reference src/*.c -O2 FILE* API, 1 thread, {cpu_model()}")
+            res["identical_to_reference"] = comp_ref == comp_gpu
+            ok = ok and r["round_trip_ok"] and comp_ref == comp_gpu
+    res["round_trip_ok"] = bool(ok)
+    return res
+
+
 def hbm_copy_gbps(dev, nbytes: int = GiB) -> float:
     """Device-to-device copy (read + write bytes) as the box's HBM check."""
     a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
@@ -348,15 +413,26 @@ def checksum(t: torch.Tensor) -> int:
     return s & ((1 << 62) - 1)
 
 
-def load_pmc(path: str, workload: str, n: int) -> dict:
-    """{kernel: hbm_bytes per launch} of a tools/pmc_summary.py file for this workload and size."""
-    try:
-        pm = json.load(open(path))
-        if pm.get("workload") == workload and pm.get("bytes_per_gpu") == n:
-            return {k: v.get("hbm_bytes") for k, v in pm["kernels"].items()}
-    except (OSError, ValueError, KeyError):
-        pass
-    return {}
+def load_pmc(path, workload: str, n: int) -> dict:
+    """{kernel: hbm_bytes per launch} from the tools/pmc_summary.py file
+    measured on this workload with launches of n input bytes (the file at
+    `path`, or the newest matching profiles/pmc_*.json)."""
+    import glob
+    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+    best = None
+    for p in cands:
+        try:
+            pm = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if pm.get("workload") == workload and pm.get("launch_bytes", pm.get("bytes_per_gpu")) == n and \
+                "kernels" in pm and (best is None or str(pm.get("round", "")) > str(best[0].get("round", ""))):
+            best = (pm, p)
+    if best is None:
+        return {}
+    out = {k: v.get("hbm_bytes") for k, v in best[0]["kernels"].items()}
+    out["_source"] = os.path.relpath(best[1], ROOT)
+    return out
 
 
 class Piece:
@@ -503,7 +579,10 @@ def kernel_report(job: Job, clen: int, k1, k3, k4, pmc: dict) -> dict:
     traffic = pmc.get(dom_name)
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-            "kernel": dom_name, "kernel_ms": round(dom_ms, 3), "algorithmic_bytes_per_launch": dom_bytes}
+            "kernel": dom_name, "kernel_ms": round(dom_ms, 3), "algorithmic_bytes_per_launch": dom_bytes,
+            "launch_bytes": kern_n}
+    if traffic is not None:
+        roof["traffic_source"] = pmc.get("_source")
     # counter bytes of each whole path (K1r + K3 + K2 write the compressed
     # bytes; K4 alone decodes) beside the same path's algorithmic bytes
     paths = {}
@@ -542,15 +621,16 @@ def sub_result(name: str, codec, dev, steps: int, warmup: int, piece_bytes: int,
     t_gen = time.perf_counter() - t_gen
     elapsed, clen, k1, k3, k4 = timed_steps(job, steps, warmup, 1)
     ok = job.verify()
-    rep = kernel_report(job, clen, k1, k3, k4, load_pmc(pmc_path(name), name, job.n if job.decode_only
-                                                          else job.pieces[-1].n))
+    rep = kernel_report(job, clen, k1, k3, k4, load_pmc(None, name, job.n if job.decode_only
+                                                        else job.pieces[-1].n))
     total_comp = clen
     job.free()
     res = {"workload": f"{name}: {n / GiB:.4g} GiB, {job.desc}", "value": round(n / (elapsed / steps) / 1e6, 1),
            "unit": "MB/s", "steps": steps, "ms_per_step": round(elapsed / steps * 1e3, 3),
            "ratio": round(n / total_comp, 4), "compress_MBps": rep["compress_MBps"],
            "decompress_MBps": rep["decompress_MBps"], "kernel_ms": rep["kernel_ms"],
-           "roofline": {k: rep["roofline"][k] for k in ("kernel", "kernel_ms", "achieved", "frac", "traffic")},
+           "roofline": {k: rep["roofline"][k] for k in ("kernel", "kernel_ms", "achieved", "frac", "traffic",
+                                                        "traffic_source", "launch_bytes") if k in rep["roofline"]},
            "round_trip_ok": ok, "setup_s": round(t_gen, 1)}
     if "path_traffic" in rep["roofline"]:
         res["roofline"]["path_traffic"] = rep["roofline"]["path_traffic"]
@@ -563,19 +643,22 @@ def sub_result(name: str, codec, dev, steps: int, warmup: int, piece_bytes: int,
 
 def resolve_sizes(args, world: int, rank: int):
     """(strong, total input bytes, this rank's offset, its bytes, the largest
-    rank's bytes).  N > 1 without size flags is configs[3] (64 GiB in total,
-    strong scaling); N = 1 without them configs[1] (1 GiB)."""
+    rank's bytes).  Without size flags: configs[3] (64 GiB in total, strong
+    scaling) for text32k at every N -- so --gpus 1/2/4/8 is one job on one
+    curve -- and for every other compressing workload at N > 1; another
+    workload alone at N = 1 is 1 GiB (decode10g: its ~10 GB stream)."""
     kind, seed, layout, chunk, desc = WORKLOADS[args.workload]
     unit = chunk if layout == snappy_amd.STREAMS else 65536
     total = args.total_bytes
-    if world > 1 and not args.weak and total == 0 and args.workload not in DECODE_ONLY:
+    weak = args.weak or args.bytes_per_gpu is not None
+    if total == 0 and not weak and args.workload not in DECODE_ONLY and (world > 1 or args.workload == "text32k"):
         total = CONFIG3_BYTES
     if total > 0:
         r_off, n = shard_range(total, world, rank, unit)
         n_max = max(shard_range(total, world, r, unit)[1] for r in range(world))
         return True, total, r_off, n, n_max
-    n = args.bytes_per_gpu
-    if args.workload in DECODE_ONLY and n == GiB and not args.keep_size:
+    n = args.bytes_per_gpu if args.bytes_per_gpu is not None else GiB
+    if args.workload in DECODE_ONLY and args.bytes_per_gpu is None and not args.keep_size:
         n = DECODE10G_BYTES
     return False, n * world, rank * n, n, n
 
@@ -662,12 +745,14 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     value = total_in / (elapsed / args.steps) / 1e6
     pmc = load_pmc(args.pmc, args.workload, job.n if decode_only else job.pieces[-1].n)
+    config3 = strong and total_in == CONFIG3_BYTES and args.workload == "text32k"
     rep = kernel_report(job, clen, k1, k3, k4, pmc)
     plan = rank_plan(total_in if strong else n * world, world, unit, args.piece_bytes,
                      exchange=world > 1 and not args.no_assemble, gather_decoded=args.c3)
     used = mem_after_steps[1] - mem_after_steps[0]
     rank_peak = torch_peak + scratch_peak
     n_units = job.units
+    launch_bytes = job.n if decode_only else job.pieces[-1].n
     job.free()
 
     line = None
@@ -681,7 +766,7 @@ def main():
             e2e = host_end_to_end(kind, seed, min(n, 256 << 20))
         size_txt = (f"{total_in / GiB:.4g} GiB in total over {world} GPU(s)" if strong else
                     f"{n / GiB:.4g} GiB/GPU")
-        cfg_name = "configs[3]" if strong and args.workload == "text32k" else \
+        cfg_name = "configs[3]" if config3 else \
             {"text32k": "configs[1]", "text64k": "configs[1] (64 KiB blocks)", "random": "configs[2]",
              "repeat": "configs[2]", "decode10g": "configs[4]"}[args.workload]
         line = {
@@ -694,7 +779,8 @@ def main():
                                                                             else "")),
                        "bytes_per_gpu": n, "total_bytes": total_in, "chunk": chunk,
                        "layout": "STREAMS" if layout else "SINGLE", "units_per_gpu": n_units,
-                       "pieces_per_gpu": len(job.pieces), "parallelism": f"dp{world} (block shards)"},
+                       "pieces_per_gpu": len(job.pieces), "launch_bytes": launch_bytes,
+                       "workload_name": args.workload, "parallelism": f"dp{world} (block shards)"},
             "roofline": rep["roofline"],
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
@@ -718,13 +804,16 @@ def main():
         if assemble:
             line["value_end_to_end"] = assemble.pop("value_end_to_end")
             line["exchange"] = assemble
-    if rank == 0 and world == 1 and not args.no_sub and args.workload == "text32k" and not strong:
+    if rank == 0 and world == 1 and not args.no_sub and config3:
         subs = {}
         sub_steps, sub_warm = max(1, min(args.steps, 10)), min(args.warmup, 2)
         for w in SUB_WORKLOADS:
             codec.trim()
             subs[w] = sub_result(w, codec, dev, sub_steps, sub_warm, args.piece_bytes, not args.no_cpu_baseline)
             ok = ok and subs[w]["round_trip_ok"]
+        codec.trim()
+        subs["config0"] = config0_file_api()
+        ok = ok and subs["config0"]["round_trip_ok"]
         line["configs"] = subs
         if not args.no_host_e2e:
             codec.trim()
@@ -741,6 +830,30 @@ def main():
         sys.exit(3)
 
 
+COMPACT_BOUNCE = 256 << 20  # dist.COMPACT_BOUNCE: the compaction's staging buffer
+
+
+def compact_in_place(full: torch.Tensor, mx: int, sz, offs, bounce: torch.Tensor) -> None:
+    """Move shard r of the padded C2 gather from r * mx down to its stream
+    offset offs[r] <= r * mx, in place: in ascending order, each piece staged
+    through `bounce` (a piece's destination can overlap its own source and
+    earlier pieces' sources, which were already read, never a later piece's),
+    so the gather buffer becomes the contiguous stream without a second
+    stream-sized buffer (dist.rank_plan)."""
+    step = bounce.numel()
+    for r in range(1, len(sz)):
+        src, dst = r * mx, int(offs[r])
+        if src == dst:
+            continue
+        for o in range(0, sz[r], step):
+            m = min(step, sz[r] - o)
+            if dst + o + m <= src + o:  # no overlap: one copy
+                full[dst + o:dst + o + m].copy_(full[src + o:src + o + m])
+            else:
+                bounce[:m].copy_(full[src + o:src + o + m])
+                full[dst + o:dst + o + m].copy_(bounce[:m])
+
+
 def end_to_end(job: Job, world: int, rank: int, args, cdev, gloo, allgather, total_in: int) -> dict:
     """The whole job as one pipeline, timed over --e2e-steps steps (max over
     ranks): compress the shard, C1 (size all-gather -> every shard's offset),
@@ -751,7 +864,7 @@ def end_to_end(job: Job, world: int, rank: int, args, cdev, gloo, allgather, tot
     per-shard checksums of the reassembled stream and the round trip."""
     dev = job.dev
     sizes = torch.zeros(world, dtype=torch.int64, device=cdev)
-    state = {"full": None, "stream": None, "mx": 0}
+    state = {"full": None, "bounce": None, "mx": 0}
 
     def step():
         clen = job.compress_all()
@@ -760,19 +873,21 @@ def end_to_end(job: Job, world: int, rank: int, args, cdev, gloo, allgather, tot
         mx = max(max(sz), 1)
         if state["full"] is None or state["full"].numel() < world * mx:
             state["full"] = None
-            state["stream"] = None
             torch.cuda.empty_cache()
             state["full"] = torch.empty(world * mx, dtype=torch.uint8, device=cdev)
-            state["stream"] = torch.empty(max(sum(sz), 1), dtype=torch.uint8, device=dev)
-        full, stream = state["full"], state["stream"]
+            state["bounce"] = torch.empty(COMPACT_BOUNCE, dtype=torch.uint8, device=cdev)
+        full, bounce = state["full"], state["bounce"]
         state["mx"] = mx
         if gloo:
             allgather(full[:world * mx], job.out[:mx].to(cdev))
         else:
             allgather(full[:world * mx], job.out[:mx])  # C2 (job.out holds >= mx bytes on every rank)
         offs = np.concatenate([[0], np.cumsum(sz)])
-        for r in range(world):  # compaction: shard r from r * mx to its stream offset
-            stream[offs[r]:offs[r] + sz[r]].copy_(full[r * mx:r * mx + sz[r]], non_blocking=True)
+        compact_in_place(full, mx, sz, offs, bounce)
+        stream = full[:int(offs[-1])]
+        if gloo:
+            stream = stream.to(dev)
+        state["stream"] = stream
         job.decompress_all(stream.data_ptr() + int(offs[rank]))
         return sz
 
@@ -807,7 +922,7 @@ def end_to_end(job: Job, world: int, rank: int, args, cdev, gloo, allgather, tot
            "stream_bytes": int(sum(sz)), "c2_padded_bytes_per_rank_out": world * mx,
            "backend": "gloo" if gloo else "nccl (RCCL)", "verified": float(flag) == 0.0,
            "torch_peak_bytes": torch_peak}
-    state["full"] = state["stream"] = None
+    state["full"] = state["stream"] = state["bounce"] = None
     torch.cuda.empty_cache()
     return res
 

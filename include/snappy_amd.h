@@ -85,6 +85,35 @@ int snappy_compress_buffer(const uint8_t *in, size_t n, uint8_t *out, size_t *ou
 int snappy_decompress_buffer(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len);
 int snappy_uncompressed_length(const uint8_t *in, size_t n, uint64_t *len);
 
+/* Threads and devices of the host-memory and FILE* calls above.  Each call
+ * leases a pooled host context (its own streams, device scratch and pinned
+ * staging) of the calling thread's device and returns it when it ends, so
+ * calls from several threads run concurrently.  The device is the one set
+ * here for the calling thread (-1: back to the default), else the
+ * SNAPPY_AMD_DEVICE environment variable (read once), else 0. */
+int snappy_amd_host_set_device(int device);
+int snappy_amd_host_get_device(void);
+/* Free every idle pooled host context (device scratch and pinned staging). */
+int snappy_amd_host_release(void);
+/* Idle host contexts in the pool (diagnostics). */
+size_t snappy_amd_host_pool_size(void);
+
+/* The host-memory API over several devices (a device may be listed more
+ * than once).  Compress: the input's 65,536-byte blocks are split into one
+ * contiguous range per device (the first range writes the preamble), each
+ * compressed on its device by its own thread; once every range's size is
+ * known (C1) each device copies its bytes to their place in out (C2).  The
+ * bytes equal snappy_compress_buffer's; out must hold
+ * snappy_max_compressed_length(n).  Decompress: the first device builds the
+ * block index, every device decodes one range of blocks from its part of the
+ * stream; a stream whose ranges are not self-contained (elements straddling a
+ * range start, copies reaching an earlier range) is decoded whole on the
+ * first device instead, so the results equal snappy_decompress_buffer's. */
+int snappy_compress_buffer_multi(const int *devices, int ndev, const uint8_t *in, size_t n, uint8_t *out,
+                                 size_t *out_len);
+int snappy_decompress_buffer_multi(const int *devices, int ndev, const uint8_t *in, size_t n, uint8_t *out,
+                                   size_t cap, size_t *out_len);
+
 /* ---- device-resident batch API (all pointers are HBM) ----------------- */
 typedef struct snappy_amd_ctx snappy_amd_ctx;
 
@@ -100,9 +129,18 @@ void *snappy_amd_get_stream(snappy_amd_ctx *ctx);
  * the largest call made and is kept. */
 size_t snappy_amd_device_bytes(snappy_amd_ctx *ctx);
 /* Release the scratch above (synchronises the context stream); the next call
- * allocates again.  Used to make room in HBM between phases (bench.py frees
- * the compressor's token lists before the all-gather of the shards). */
+ * allocates again.  The status words of a decode whose status has not been
+ * read yet (decompress_device_async) are kept until it is read.  Used to make
+ * room in HBM between phases (bench.py trims before C3, the all-gather of the
+ * decoded shards, and between its sub-workloads). */
 int snappy_amd_trim(snappy_amd_ctx *ctx);
+
+/* Options of a context (snappy_amd_set_option). */
+#define SNAPPY_AMD_OPT_SERIAL_INDEX 1 /* 1: index_device walks the stream with one wave
+                                         (the chunk-parallel K5p pass otherwise) */
+#define SNAPPY_AMD_OPT_K1R_EXTRA_LDS 2 /* bytes of extra dynamic LDS per K1r unit
+                                          (occupancy experiments; default 0) */
+int snappy_amd_set_option(snappy_amd_ctx *ctx, int option, int64_t value);
 
 /* Number of units (blocks or streams) for n bytes in a layout. */
 size_t snappy_amd_num_units(size_t n, uint32_t chunk, int layout);

@@ -9,6 +9,7 @@
 #include <string.h>
 #include <algorithm>
 #include <fcntl.h>
+#include <memory>
 #include <mutex>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -51,6 +52,8 @@ struct snappy_amd_ctx {
     uint8_t *k5buf = nullptr; size_t k5buf_cap = 0;  // chunk-parallel index scratch
     uint8_t *k5copy = nullptr; size_t k5copy_cap = 0;  // aligned copy of a misaligned stream
     bool timing = false;
+    bool serial_index = false;  // SNAPPY_AMD_OPT_SERIAL_INDEX
+    uint32_t k1r_extra_lds = 0; // SNAPPY_AMD_OPT_K1R_EXTRA_LDS
     hipEvent_t ev[5] = {};
     float k1_ms = 0, k3_ms = 0, k4_ms = 0;
 };
@@ -128,15 +131,37 @@ int snappy_amd_trim(snappy_amd_ctx *c)
     if (c->stream) HIP_OK(hipStreamSynchronize(c->stream));
     struct { void **p; size_t *cap; } bufs[] = {
         {reinterpret_cast<void **>(&c->tokens), &c->tokens_cap}, {reinterpret_cast<void **>(&c->seg_off), &c->seg_off_cap},
+        {reinterpret_cast<void **>(&c->ntok), &c->ntok_cap}, {reinterpret_cast<void **>(&c->sizes), &c->sizes_cap},
         {reinterpret_cast<void **>(&c->d_a), &c->d_a_cap}, {reinterpret_cast<void **>(&c->d_b), &c->d_b_cap},
         {reinterpret_cast<void **>(&c->d_idx), &c->d_idx_cap}, {reinterpret_cast<void **>(&c->k5buf), &c->k5buf_cap},
-        {reinterpret_cast<void **>(&c->k5copy), &c->k5copy_cap}};
+        {reinterpret_cast<void **>(&c->k5copy), &c->k5copy_cap},
+        // a decode's status words only until its status has been read
+        {reinterpret_cast<void **>(&c->status), c->last_units ? nullptr : &c->status_cap}};
     for (auto &b : bufs) {
+        if (!b.cap) continue;
         if (*b.p) (void)hipFree(*b.p);
         *b.p = nullptr;
         *b.cap = 0;
     }
+    if (!c->last_units && c->h_status) {
+        (void)hipHostFree(c->h_status);
+        c->h_status = nullptr;
+        c->h_status_cap = 0;
+    }
     return SNAPPY_AMD_OK;
+}
+
+int snappy_amd_set_option(snappy_amd_ctx *c, int option, int64_t value)
+{
+    if (!c) return SNAPPY_AMD_ERR_ARG;
+    switch (option) {
+    case SNAPPY_AMD_OPT_SERIAL_INDEX: c->serial_index = value != 0; return SNAPPY_AMD_OK;
+    case SNAPPY_AMD_OPT_K1R_EXTRA_LDS:
+        if (value < 0 || value > 65536) return SNAPPY_AMD_ERR_ARG;
+        c->k1r_extra_lds = (uint32_t)value;
+        return SNAPPY_AMD_OK;
+    default: return SNAPPY_AMD_ERR_ARG;
+    }
 }
 
 int snappy_amd_set_stream(snappy_amd_ctx *c, void *s)
@@ -224,10 +249,10 @@ static int compress_impl(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t
         return rc;
     const uint32_t hm = hdr_mode_of(layout, flags);
     if (c->timing) (void)hipEventRecord(c->ev[0], c->stream);
-    // units <= 32 KiB: unit in VGPRs (3 waves/SIMD); 64 KiB blocks: VGPRs + AGPRs (1 wave/SIMD)
-    // SNAPPY_K1R_DYNLDS=<bytes>: occupancy experiments (extra dynamic LDS per unit)
-    const char *dyn = getenv("SNAPPY_K1R_DYNLDS");
-    const uint32_t dyn_lds = dyn ? (uint32_t)atoi(dyn) : 0;
+    // units <= 32 KiB: the unit in 128 VGPRs; 65,536-byte blocks: its last 128
+    // segments in a 128-VGPR ring fed by LDS-DMA (both 3 waves/SIMD).
+    // Extra dynamic LDS per unit: occupancy experiments only (SNAPPY_AMD_OPT_K1R_EXTRA_LDS)
+    const uint32_t dyn_lds = c->k1r_extra_lds;
     if (unit <= SNAPPY_K1R_MAX_UNIT)
         hipLaunchKernelGGL(k1r_match_units, dim3((uint32_t)units), dim3(64), dyn_lds, c->stream,
                            static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens,
@@ -368,7 +393,7 @@ int snappy_amd_index_device(snappy_amd_ctx *c, const void *d_comp, size_t clen, 
     if (!c || !d_comp || !d_offsets) return SNAPPY_AMD_ERR_ARG;
     HIP_OK(hipSetDevice(c->device));
     const uint8_t *comp = static_cast<const uint8_t *>(d_comp);
-    const bool serial = getenv("SNAPPY_AMD_K5_SERIAL") != nullptr;  // read per call (tests toggle it)
+    const bool serial = c->serial_index;
     if (!serial && clen >= 4 * (size_t)K5_CHUNK && (reinterpret_cast<uintptr_t>(d_comp) & 3)) {
         // K5p stages 4-aligned dwords of the stream: a stream at an odd address
         // is first moved to an aligned scratch copy (one HBM pass, a few % of
@@ -415,51 +440,8 @@ int snappy_amd_index_device(snappy_amd_ctx *c, const void *d_comp, size_t clen, 
     return (int)res[0];
 }
 
-// ---- host-buffer helpers (used by snappy_host.c) -------------------------
-
-static std::mutex g_mu;
-static snappy_amd_ctx *g_ctx = nullptr;
-
-static int global_ctx(snappy_amd_ctx **out)
-{
-    if (!g_ctx) {
-        int dev = 0;
-        const char *e = getenv("SNAPPY_AMD_DEVICE");
-        if (e) dev = atoi(e);
-        int rc = snappy_amd_create(dev, &g_ctx);
-        if (rc) { g_ctx = nullptr; return rc; }
-    }
-    *out = g_ctx;
-    return SNAPPY_AMD_OK;
-}
-
-int snappy_amd_host_compress(const uint8_t *in, size_t n, uint64_t header_value, uint8_t *out, size_t cap,
-                             size_t *out_len)
-{
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (!out_len || (!in && n)) return SNAPPY_AMD_ERR_ARG;
-    *out_len = 0;
-    if (n == 0) return SNAPPY_AMD_OK;
-    snappy_amd_ctx *c;
-    int rc = global_ctx(&c);
-    if (rc) return rc;
-    HIP_OK(hipSetDevice(c->device));
-    const size_t units = (n + SNAPPY_AMD_BLOCK - 1) / SNAPPY_AMD_BLOCK;
-    const size_t maxo = snappy_amd_max_output(n, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE);
-    if ((rc = grow(reinterpret_cast<void **>(&c->d_a), &c->d_a_cap, n + 16))) return rc;
-    if ((rc = grow(reinterpret_cast<void **>(&c->d_b), &c->d_b_cap, maxo))) return rc;
-    if ((rc = grow(reinterpret_cast<void **>(&c->d_idx), &c->d_idx_cap, (units + 1) * sizeof(uint64_t)))) return rc;
-    HIP_OK(hipMemcpyAsync(c->d_a, in, n, hipMemcpyHostToDevice, c->stream));
-    size_t len = 0;
-    rc = compress_impl(c, c->d_a, n, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE, 0, header_value, c->d_b, c->d_idx, &len);
-    if (rc) return rc;
-    if (len > cap) return SNAPPY_AMD_ERR_CAPACITY;
-    HIP_OK(hipMemcpyAsync(out, c->d_b, len, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
-    *out_len = len;
-    return SNAPPY_AMD_OK;
-}
-
+// ---- host-buffer and FILE* paths (used by snappy_host.c) -------------------
+//
 // Streaming FILE* compress: the reference's fread/compress/
 // fwrite block loop (snappy_compression.c:419-425) as a two-slot pipeline of
 // 64 MiB chunks (a multiple of the 65,536-byte block, so block boundaries and
@@ -479,7 +461,6 @@ struct StreamSlot {
     bool busy = false;
 };
 constexpr size_t kStreamChunk = (size_t)64 << 20;
-StreamSlot g_slots[2];
 
 size_t read_full(FILE *f, uint8_t *b, size_t cap)
 {
@@ -501,9 +482,8 @@ double io_now()
 }
 bool io_trace()
 {
-    static int on = -1;
-    if (on < 0) on = getenv("SNAPPY_AMD_IO_TRACE") != nullptr;
-    return on > 0;
+    static const bool on = getenv("SNAPPY_AMD_IO_TRACE") != nullptr;  // read once
+    return on;
 }
 
 // Threads copying file chunks between the page cache and pinned staging:
@@ -783,11 +763,198 @@ int slot_drain(StreamSlot &s, AsyncWriter &wr, IoFile &fout, FILE *fidx, uint64_
     *base += len;
     return SNAPPY_AMD_OK;
 }
+
+// pinned staging of the FILE* decoder: 3 chunks in rotation (one being
+// filled or drained by the host threads while the copy engine moves another)
+struct DecStage {
+    uint8_t *h[3] = {};
+    hipEvent_t ev[3] = {};
+    bool ready = false;
+};
+
+void dec_stage_free(DecStage &d)
+{
+    for (int j = 0; j < 3; j++) {
+        if (d.h[j]) (void)hipHostFree(d.h[j]);
+        if (d.ev[j]) (void)hipEventDestroy(d.ev[j]);
+        d.h[j] = nullptr;
+        d.ev[j] = nullptr;
+    }
+    d.ready = false;
+}
+
+int dec_stage_init(DecStage &d)
+{
+    if (d.ready) return SNAPPY_AMD_OK;
+    for (int i = 0; i < 3; i++) {
+        if (hipHostMalloc(&d.h[i], kStreamChunk, hipHostMallocDefault) != hipSuccess ||
+            hipEventCreateWithFlags(&d.ev[i], hipEventDisableTiming) != hipSuccess) {
+            dec_stage_free(d);
+            return SNAPPY_AMD_ERR_DEVICE;
+        }
+    }
+    d.ready = true;
+    return SNAPPY_AMD_OK;
+}
+
+// Host calls (host-buffer and FILE* APIs) run on pooled host contexts: a call
+// leases an idle context of its device (or creates one) and returns it at the
+// end, so concurrent calls from several threads run concurrently, each on its
+// own streams, scratch and pinned staging.  The pool's lock is held only to
+// take or return a context.  The device is the calling thread's
+// (snappy_amd_host_set_device), else SNAPPY_AMD_DEVICE (read once), else 0.
+struct HostCtx {
+    int device = 0;
+    snappy_amd_ctx *c = nullptr;  // host-buffer path and the FILE* decoder
+    StreamSlot slots[2];          // the FILE* compressor's two pipeline slots
+    DecStage dec;                 // the FILE* decoder's pinned staging
+};
+
+void host_free(HostCtx *h)
+{
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    for (auto &s : h->slots) slot_free(s);
+    dec_stage_free(h->dec);
+    snappy_amd_destroy(h->c);
+    delete h;
+}
+
+std::mutex g_pool_mu;
+std::vector<HostCtx *> g_pool;  // idle host contexts, any device
+thread_local int t_host_device = -1;
+
+int default_device()
+{
+    static const int d = [] {
+        const char *e = getenv("SNAPPY_AMD_DEVICE");
+        return e ? atoi(e) : 0;
+    }();
+    return d;
+}
+
+int host_device() { return t_host_device >= 0 ? t_host_device : default_device(); }
+
+class Lease {
+public:
+    explicit Lease(int device)
+    {
+        {
+            std::lock_guard<std::mutex> lk(g_pool_mu);
+            for (size_t i = g_pool.size(); i-- > 0;)
+                if (g_pool[i]->device == device) {
+                    h_ = g_pool[i];
+                    g_pool.erase(g_pool.begin() + (long)i);
+                    break;
+                }
+        }
+        if (!h_) {
+            HostCtx *h = new HostCtx();
+            h->device = device;
+            rc_ = snappy_amd_create(device, &h->c);
+            if (rc_) delete h;
+            else h_ = h;
+        }
+        if (h_ && hipSetDevice(device) != hipSuccess) rc_ = SNAPPY_AMD_ERR_DEVICE;
+    }
+    ~Lease()
+    {
+        if (!h_) return;
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        g_pool.push_back(h_);
+    }
+    Lease(const Lease &) = delete;
+    Lease &operator=(const Lease &) = delete;
+    int rc() const { return rc_; }
+    HostCtx &operator*() const { return *h_; }
+    HostCtx *operator->() const { return h_; }
+
+private:
+    HostCtx *h_ = nullptr;
+    int rc_ = SNAPPY_AMD_OK;
+};
+
+// one SINGLE-layout stream (or, with NO_PREAMBLE, a block-aligned part of
+// one) of in[0..n) on host context h: H2D, kernels, the compressed bytes left
+// in h.c->d_b and the block index in h.c->d_idx; *len = compressed bytes
+int host_compress_stage(HostCtx &h, const uint8_t *in, size_t n, uint32_t flags, uint64_t header_value, size_t *len)
+{
+    snappy_amd_ctx *c = h.c;
+    const size_t units = (n + SNAPPY_AMD_BLOCK - 1) / SNAPPY_AMD_BLOCK;
+    const size_t maxo = snappy_amd_max_output(n, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE);
+    int rc;
+    if ((rc = grow(reinterpret_cast<void **>(&c->d_a), &c->d_a_cap, n + 16))) return rc;
+    if ((rc = grow(reinterpret_cast<void **>(&c->d_b), &c->d_b_cap, maxo))) return rc;
+    if ((rc = grow(reinterpret_cast<void **>(&c->d_idx), &c->d_idx_cap, (units + 1) * sizeof(uint64_t)))) return rc;
+    HIP_OK(hipMemcpyAsync(c->d_a, in, n, hipMemcpyHostToDevice, c->stream));
+    return compress_impl(c, c->d_a, n, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE, flags, header_value, c->d_b, c->d_idx, len);
+}
+
+// a sidecar index must describe the stream: every entry inside it, never
+// decreasing, the last one its length (a tampered .idx is refused here)
+bool index_fits(const uint64_t *idx, size_t count, size_t units, uint64_t clen)
+{
+    const uint64_t off_mask = (1ull << SNAPPY_AMD_IDX_OFFSET_BITS) - 1;
+    if (count != units + 1 || (idx[units] & off_mask) != clen) return false;
+    for (size_t i = 0; i < units; i++)
+        if ((idx[i] & off_mask) > (idx[i + 1] & off_mask)) return false;
+    return true;
+}
+
+// the largest output a valid stream of n compressed bytes can declare: a
+// 3-byte copy-2 element writes at most 64 bytes (src/snappy_decompression.c:
+// 290-333), so no stream expands by more than 64/3; a preamble promising more
+// is a truncated stream, refused before any output is allocated or mapped
+bool length_plausible(uint64_t N, uint64_t n) { return N / 22 <= n; }
 }  // namespace
+
+int snappy_amd_host_set_device(int device)
+{
+    int count = 0;
+    if (device >= 0 && (hipGetDeviceCount(&count) != hipSuccess || device >= count)) return SNAPPY_AMD_ERR_DEVICE;
+    t_host_device = device < 0 ? -1 : device;
+    return SNAPPY_AMD_OK;
+}
+
+int snappy_amd_host_get_device(void) { return host_device(); }
+
+int snappy_amd_host_release(void)
+{
+    std::vector<HostCtx *> idle;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        idle.swap(g_pool);
+    }
+    for (HostCtx *h : idle) host_free(h);
+    return SNAPPY_AMD_OK;
+}
+
+size_t snappy_amd_host_pool_size(void)
+{
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    return g_pool.size();
+}
+
+int snappy_amd_host_compress(const uint8_t *in, size_t n, uint64_t header_value, uint8_t *out, size_t cap,
+                             size_t *out_len)
+{
+    if (!out_len || (!in && n)) return SNAPPY_AMD_ERR_ARG;
+    *out_len = 0;
+    if (n == 0) return SNAPPY_AMD_OK;
+    Lease h(host_device());
+    if (h.rc()) return h.rc();
+    size_t len = 0;
+    int rc = host_compress_stage(*h, in, n, 0, header_value, &len);
+    if (rc) return rc;
+    if (len > cap) return SNAPPY_AMD_ERR_CAPACITY;
+    HIP_OK(hipMemcpyAsync(out, h->c->d_b, len, hipMemcpyDeviceToHost, h->c->stream));
+    HIP_OK(hipStreamSynchronize(h->c->stream));
+    *out_len = len;
+    return SNAPPY_AMD_OK;
+}
 
 int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, FILE *fidx, uint64_t *bytes_in)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
     if (!fin || !fout) return SNAPPY_AMD_ERR_ARG;
     uint64_t base = 0;  // stream bytes written so far
     long idx_hdr = -1;
@@ -796,8 +963,10 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
         const uint64_t h[3] = {SNAPPY_AMD_IDX_MAGIC, header_value, 0};
         if (idx_hdr < 0 || fwrite(h, sizeof(uint64_t), 3, fidx) != 3) return SNAPPY_AMD_ERR_IO;
     }
-    int dev = 0;
-    if (const char *e = getenv("SNAPPY_AMD_DEVICE")) dev = atoi(e);
+    const int dev = host_device();
+    Lease hc(dev);
+    if (hc.rc()) return hc.rc();
+    StreamSlot *slots = hc->slots;
     IoFile in, out;
     AsyncWriter wr;  // (declared after out: joined before out is destroyed)
     if (!in.open(fin, false) || !out.open(fout, true)) return SNAPPY_AMD_ERR_IO;
@@ -805,7 +974,8 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
     // 8 faulting threads, 0.59 -> 0.77 s of writes for 2.3 GB on the GPU box's tmpfs)
     const bool out_mapped = false;
     int rc;
-    for (auto &s : g_slots) {
+    for (int i = 0; i < 2; i++) {
+        StreamSlot &s = slots[i];
         if ((rc = slot_init(s, dev))) return rc;
         if (s.busy) {  // left over by a failed call: discard
             (void)hipStreamSynchronize(s.c->stream);
@@ -816,12 +986,12 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
     uint64_t total_in = 0;
     const double t0 = io_now();
     double t_rd = 0, t_dr = 0;
-    size_t n = in.read(g_slots[0].h_in, kStreamChunk);
+    size_t n = in.read(slots[0].h_in, kStreamChunk);
     t_rd += io_now() - t0;
     if (in.error()) return SNAPPY_AMD_ERR_IO;
     for (uint32_t k = 0; n > 0; k++) {
-        StreamSlot &s = g_slots[k & 1];
-        StreamSlot &o = g_slots[(k + 1) & 1];
+        StreamSlot &s = slots[k & 1];
+        StreamSlot &o = slots[(k + 1) & 1];
         s.n = n;
         total_in += n;
         HIP_OK(hipMemcpyAsync(s.d_in, s.h_in, n, hipMemcpyHostToDevice, s.c->stream));
@@ -842,8 +1012,8 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
     }
     // the slots drain in chunk order: the one holding the last chunk goes last
     const uint32_t last = total_in ? (uint32_t)(((total_in + kStreamChunk - 1) / kStreamChunk - 1) & 1) : 0;
-    if ((rc = slot_drain(g_slots[last ^ 1], wr, out, fidx, &base))) return rc;
-    if ((rc = slot_drain(g_slots[last], wr, out, fidx, &base))) return rc;
+    if ((rc = slot_drain(slots[last ^ 1], wr, out, fidx, &base))) return rc;
+    if ((rc = slot_drain(slots[last], wr, out, fidx, &base))) return rc;
     wr.wait();
     if (!wr.ok) return SNAPPY_AMD_ERR_IO;
     if (!in.finish() || !out.finish()) return SNAPPY_AMD_ERR_IO;
@@ -877,29 +1047,24 @@ int snappy_amd_host_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t
 int snappy_amd_host_decompress_idx(const uint8_t *in, size_t n, const uint64_t *idx, size_t count, uint8_t *out,
                                    size_t cap, size_t *out_len)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
     if (!out_len || (!in && n)) return SNAPPY_AMD_ERR_ARG;
     *out_len = 0;
     if (n == 0) return SNAPPY_AMD_OK;
     uint64_t N = 0;
     if (snappy_varint_decode(in, n, &N) == 0) return SNAPPY_AMD_ERR_HEADER;
     if (N > cap) return SNAPPY_AMD_ERR_CAPACITY;
-    snappy_amd_ctx *c;
-    int rc = global_ctx(&c);
-    if (rc) return rc;
-    HIP_OK(hipSetDevice(c->device));
+    if (!length_plausible(N, n)) return SNAPPY_AMD_ERR_TRUNCATED;
+    Lease h(host_device());
+    if (h.rc()) return h.rc();
+    snappy_amd_ctx *c = h->c;
     const size_t units = (N + SNAPPY_AMD_BLOCK - 1) / SNAPPY_AMD_BLOCK;
+    int rc;
     if ((rc = grow(reinterpret_cast<void **>(&c->d_a), &c->d_a_cap, n + 16))) return rc;
     if ((rc = grow(reinterpret_cast<void **>(&c->d_b), &c->d_b_cap, N + 16))) return rc;
     if ((rc = grow(reinterpret_cast<void **>(&c->d_idx), &c->d_idx_cap, (units + 2) * sizeof(uint64_t)))) return rc;
     HIP_OK(hipMemcpyAsync(c->d_a, in, n, hipMemcpyHostToDevice, c->stream));
     if (idx) {  // a sidecar index: no index pass; it must describe this stream
-        // every entry, not just the last: offsets inside the stream, never
-        // decreasing, ending at its length (a tampered .idx is refused here)
-        const uint64_t off_mask = (1ull << SNAPPY_AMD_IDX_OFFSET_BITS) - 1;
-        if (count != units + 1 || (idx[units] & off_mask) != n) return SNAPPY_AMD_ERR_INDEX;
-        for (size_t i = 0; i < units; i++)
-            if ((idx[i] & off_mask) > (idx[i + 1] & off_mask)) return SNAPPY_AMD_ERR_INDEX;
+        if (!index_fits(idx, count, units, n)) return SNAPPY_AMD_ERR_INDEX;
         HIP_OK(hipMemcpyAsync(c->d_idx, idx, count * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
     } else {
         size_t got = 0;
@@ -915,49 +1080,19 @@ int snappy_amd_host_decompress_idx(const uint8_t *in, size_t n, const uint64_t *
     return SNAPPY_AMD_OK;
 }
 
-// pinned staging of the FILE* decoder: 3 chunks in rotation (one being
-// filled or drained by the host threads while the copy engine moves another)
-namespace {
-struct DecStage {
-    uint8_t *h[3] = {};
-    hipEvent_t ev[3] = {};
-    bool ready = false;
-};
-DecStage g_dec;
-
-int dec_stage_init()
-{
-    if (g_dec.ready) return SNAPPY_AMD_OK;
-    for (int i = 0; i < 3; i++) {
-        if (hipHostMalloc(&g_dec.h[i], kStreamChunk, hipHostMallocDefault) != hipSuccess ||
-            hipEventCreateWithFlags(&g_dec.ev[i], hipEventDisableTiming) != hipSuccess) {
-            for (int j = 0; j <= i; j++) {
-                if (g_dec.h[j]) (void)hipHostFree(g_dec.h[j]);
-                if (g_dec.ev[j]) (void)hipEventDestroy(g_dec.ev[j]);
-                g_dec.h[j] = nullptr;
-                g_dec.ev[j] = nullptr;
-            }
-            return SNAPPY_AMD_ERR_DEVICE;
-        }
-    }
-    g_dec.ready = true;
-    return SNAPPY_AMD_OK;
-}
-}  // namespace
-
 int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count, FILE *fout)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
     if (!fin || !fout) return SNAPPY_AMD_ERR_ARG;
     IoFile in, out;
     if (!in.open(fin, false) || !in.pos_io) return SNAPPY_AMD_ERR_UNSUPPORTED;
     const uint64_t n = in.remaining();
     if (n == 0) return in.finish() ? SNAPPY_AMD_OK : SNAPPY_AMD_ERR_IO;  // nothing to decode, nothing written
-    snappy_amd_ctx *c;
-    int rc = global_ctx(&c);
-    if (rc) return rc;
-    if ((rc = dec_stage_init())) return rc;
-    HIP_OK(hipSetDevice(c->device));
+    Lease h(host_device());
+    if (h.rc()) return h.rc();
+    snappy_amd_ctx *c = h->c;
+    DecStage &dec = h->dec;
+    int rc;
+    if ((rc = dec_stage_init(dec))) return rc;
     if ((rc = grow(reinterpret_cast<void **>(&c->d_a), &c->d_a_cap, n + 16))) return rc;
     // the output's pages are allocated (file size unchanged) from the moment
     // the header gives N, while the input is read and the index and decode
@@ -966,11 +1101,24 @@ int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count
     // inode, so this is the overlap there is).  Best effort: a file system
     // without fallocate just skips it.
     if (!out.open(fout, true)) return SNAPPY_AMD_ERR_IO;
-    std::thread prealloc;
-    struct Joiner {
-        std::thread &t;
-        ~Joiner() { if (t.joinable()) t.join(); }
-    } join_prealloc{prealloc};
+    // On any failure after the preallocation started, the blocks it added past
+    // the file's old end and past what was written are released (they are
+    // invisible in the file size); the thread is joined first.  Declared after
+    // `out`, so this runs before out's unmap / truncation.
+    struct Prealloc {
+        IoFile &out;
+        std::thread t;
+        uint64_t at = 0, len = 0, old_size = 0;
+        bool ok = false;
+        ~Prealloc()
+        {
+            if (t.joinable()) t.join();
+            if (ok || !len) return;
+            const uint64_t from = std::max(std::max(at, old_size), out.pos), end = at + len;
+            if (end > from)
+                (void)fallocate(out.fd, FALLOC_FL_PUNCH_HOLE | FALLOC_FL_KEEP_SIZE, (off_t)from, (off_t)(end - from));
+        }
+    } pre{out};
     // (1) file -> pinned chunk k % 3 (host threads) -> HBM (copy engine), the
     // next chunk read while this one is copied
     const double t0 = io_now();
@@ -980,23 +1128,30 @@ int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count
     const uint64_t nch = (n + kStreamChunk - 1) / kStreamChunk;
     for (uint64_t k = 0; k < nch; k++) {
         const int s = (int)(k % 3);
-        if (k >= 3) HIP_OK(hipEventSynchronize(g_dec.ev[s]));
+        if (k >= 3) HIP_OK(hipEventSynchronize(dec.ev[s]));
         const size_t m = (size_t)std::min<uint64_t>(kStreamChunk, n - k * kStreamChunk);
         const double tr = io_now();
-        if (in.read(g_dec.h[s], m) != m) return SNAPPY_AMD_ERR_IO;
+        if (in.read(dec.h[s], m) != m) return SNAPPY_AMD_ERR_IO;
         t_rd += io_now() - tr;
         if (k == 0) {
-            if (snappy_varint_decode(g_dec.h[0], m, &N) == 0) return SNAPPY_AMD_ERR_HEADER;
+            if (snappy_varint_decode(dec.h[0], m, &N) == 0) return SNAPPY_AMD_ERR_HEADER;
+            // N is untrusted until the decode succeeds: bounded by what n bytes
+            // can expand to before the output is mapped or preallocated
+            if (!length_plausible(N, n)) return SNAPPY_AMD_ERR_TRUNCATED;
             if (out.pos_io && N) {
+                struct stat st;
+                pre.old_size = fstat(out.fd, &st) == 0 ? (uint64_t)st.st_size : 0;
+                pre.at = out.pos;
+                pre.len = N;
                 // map first: its ftruncate would wait for the whole fallocate (both take the inode lock)
                 out_mapped = out.map_out(N);
-                prealloc = std::thread([fd = out.fd, at = out.pos, N] {
+                pre.t = std::thread([fd = out.fd, at = out.pos, N] {
                     (void)fallocate(fd, FALLOC_FL_KEEP_SIZE, (off_t)at, (off_t)N);
                 });
             }
         }
-        HIP_OK(hipMemcpyAsync(c->d_a + k * kStreamChunk, g_dec.h[s], m, hipMemcpyHostToDevice, c->stream));
-        HIP_OK(hipEventRecord(g_dec.ev[s], c->stream));
+        HIP_OK(hipMemcpyAsync(c->d_a + k * kStreamChunk, dec.h[s], m, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(hipEventRecord(dec.ev[s], c->stream));
     }
     if (!in.finish()) return SNAPPY_AMD_ERR_IO;
     const double t1 = io_now();
@@ -1005,16 +1160,16 @@ int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count
     if ((rc = grow(reinterpret_cast<void **>(&c->d_b), &c->d_b_cap, N + 16))) return rc;
     if ((rc = grow(reinterpret_cast<void **>(&c->d_idx), &c->d_idx_cap, (units + 2) * sizeof(uint64_t)))) return rc;
     if (idx) {
-        const uint64_t off_mask = (1ull << SNAPPY_AMD_IDX_OFFSET_BITS) - 1;
-        if (count != units + 1 || (idx[units] & off_mask) != n) return SNAPPY_AMD_ERR_INDEX;
-        for (uint64_t i = 0; i < units; i++)
-            if ((idx[i] & off_mask) > (idx[i + 1] & off_mask)) return SNAPPY_AMD_ERR_INDEX;
+        if (!index_fits(idx, count, units, n)) return SNAPPY_AMD_ERR_INDEX;
         HIP_OK(hipMemcpyAsync(c->d_idx, idx, count * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
     } else {
         size_t got = 0;
         if ((rc = snappy_amd_index_device(c, c->d_a, n, c->d_idx, units + 1, &got))) return rc;
     }
-    if (N == 0) return SNAPPY_AMD_OK;
+    if (N == 0) {
+        pre.ok = true;
+        return SNAPPY_AMD_OK;
+    }
     if ((rc = snappy_amd_decompress_device(c, c->d_a, c->d_idx, (size_t)N, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE,
                                            c->d_b)))
         return rc;
@@ -1024,28 +1179,28 @@ int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count
     double t_wr = 0;
     // the mapped writers need not wait for the preallocation: a page it has not
     // reached yet is allocated by the writer's populate (the preallocation skips it)
-    if (!out_mapped && prealloc.joinable()) prealloc.join();
+    if (!out_mapped && pre.t.joinable()) pre.t.join();
     const double t3 = io_now();
     const uint64_t och = (N + kStreamChunk - 1) / kStreamChunk;
     auto down = [&](uint64_t k) -> int {
         const size_t m = (size_t)std::min<uint64_t>(kStreamChunk, N - k * kStreamChunk);
-        HIP_OK(hipMemcpyAsync(g_dec.h[k % 3], c->d_b + k * kStreamChunk, m, hipMemcpyDeviceToHost, c->stream));
-        HIP_OK(hipEventRecord(g_dec.ev[k % 3], c->stream));
+        HIP_OK(hipMemcpyAsync(dec.h[k % 3], c->d_b + k * kStreamChunk, m, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipEventRecord(dec.ev[k % 3], c->stream));
         return SNAPPY_AMD_OK;
     };
     // two chunks copied down ahead of the one being written (by the writer thread:
     // chunk k's slot is refilled with chunk k + 3 once its write has been joined)
     if ((rc = down(0))) return rc;
     if (och > 1 && (rc = down(1))) return rc;
-    AsyncWriter wr;  // (after out: joined before out is destroyed)
+    AsyncWriter wr;  // (after out and pre: joined before either is destroyed)
     double t_ev = 0, t_join = 0;
     for (uint64_t k = 0; k < och; k++) {
         const double te = io_now();
-        HIP_OK(hipEventSynchronize(g_dec.ev[k % 3]));
+        HIP_OK(hipEventSynchronize(dec.ev[k % 3]));
         const size_t m = (size_t)std::min<uint64_t>(kStreamChunk, N - k * kStreamChunk);
         const double tj = io_now();
         t_ev += tj - te;
-        const bool started = wr.start(out, g_dec.h[k % 3], m);  // joins chunk k - 1's write
+        const bool started = wr.start(out, dec.h[k % 3], m);  // joins chunk k - 1's write
         t_join += io_now() - tj;
         if (!started) return SNAPPY_AMD_ERR_IO;
         if (k + 2 < och && (rc = down(k + 2))) return rc;                 // into chunk k - 1's slot
@@ -1054,6 +1209,7 @@ int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count
     t_wr = wr.busy;
     if (!wr.ok) return SNAPPY_AMD_ERR_IO;
     const bool fin_ok = out.finish();
+    pre.ok = fin_ok;
     if (io_trace())
         fprintf(stderr, "[snappy_amd io] decompress %llu -> %llu B: in %.3f s (reads %.3f), index+decode %.3f s, "
                         "preallocation wait %.3f s, out %.3f s (copy waits %.3f, writer waits %.3f, writes %.3f), "
@@ -1064,5 +1220,183 @@ int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count
     return fin_ok ? SNAPPY_AMD_OK : SNAPPY_AMD_ERR_IO;
 }
 
+// ---- several devices from one host call (SURVEY 8(e) for C callers) -------
+//
+// The host-buffer API over a list of devices: the 65,536-byte blocks of the
+// input are split into contiguous ranges, one per device (rounded up as
+// dist.shard_range: the first device holds the first block and writes the
+// preamble, the others compress with SNAPPY_AMD_NO_PREAMBLE), each compressed
+// on its device by its own thread and host context; once every size is known
+// (the C1 step) each device copies its bytes to their final offset in `out`
+// (the C2 step: the gather is the host buffer).  The output is byte-identical
+// to snappy_compress_buffer's.  A device may appear more than once (two
+// contexts on one device, as the tests do on a 1-GPU box).
 }  // extern "C"
 
+namespace {
+struct Shard {
+    size_t u0 = 0, u1 = 0;
+};
+std::vector<Shard> split_units(size_t units, int parts)
+{
+    std::vector<Shard> s((size_t)parts);
+    for (int r = 0; r < parts; r++) {
+        s[(size_t)r].u0 = (units * (size_t)r + (size_t)parts - 1) / (size_t)parts;
+        s[(size_t)r].u1 = (units * (size_t)(r + 1) + (size_t)parts - 1) / (size_t)parts;
+    }
+    return s;
+}
+
+template <class F>
+void on_threads(int parts, F f)
+{
+    std::vector<std::thread> th;
+    for (int r = 1; r < parts; r++) th.emplace_back(f, r);
+    f(0);
+    for (auto &t : th) t.join();
+}
+}  // namespace
+
+extern "C" {
+
+int snappy_compress_buffer_multi(const int *devices, int ndev, const uint8_t *in, size_t n, uint8_t *out,
+                                 size_t *out_len)
+{
+    if (!out_len || !devices || ndev < 1 || (n && (!in || !out))) return SNAPPY_AMD_ERR_ARG;
+    *out_len = 0;
+    if (n == 0) return SNAPPY_AMD_OK;
+    const size_t units = (n + SNAPPY_AMD_BLOCK - 1) / SNAPPY_AMD_BLOCK;
+    const int parts = (int)std::min<size_t>((size_t)ndev, units);
+    const std::vector<Shard> sh = split_units(units, parts);
+    std::vector<std::unique_ptr<Lease>> lease((size_t)parts);
+    for (int r = 0; r < parts; r++) {
+        lease[(size_t)r].reset(new Lease(devices[r]));
+        if (lease[(size_t)r]->rc()) return lease[(size_t)r]->rc();
+    }
+    std::vector<size_t> len((size_t)parts, 0);
+    std::vector<int> rc((size_t)parts, SNAPPY_AMD_OK);
+    on_threads(parts, [&](int r) {  // compress every range on its device
+        const size_t off = sh[(size_t)r].u0 * SNAPPY_AMD_BLOCK;
+        const size_t m = std::min(n, sh[(size_t)r].u1 * SNAPPY_AMD_BLOCK) - off;
+        HostCtx &h = **lease[(size_t)r];
+        if (hipSetDevice(h.device) != hipSuccess) { rc[(size_t)r] = SNAPPY_AMD_ERR_DEVICE; return; }
+        rc[(size_t)r] = host_compress_stage(h, in + off, m, r ? SNAPPY_AMD_NO_PREAMBLE : 0, (uint64_t)n,
+                                            &len[(size_t)r]);
+    });
+    for (int r = 0; r < parts; r++)
+        if (rc[(size_t)r]) return rc[(size_t)r];
+    std::vector<size_t> at((size_t)parts + 1, 0);  // C1: each range's offset in the stream
+    for (int r = 0; r < parts; r++) at[(size_t)r + 1] = at[(size_t)r] + len[(size_t)r];
+    if (at[(size_t)parts] > snappy_max_compressed_length(n)) return SNAPPY_AMD_ERR_CAPACITY;
+    on_threads(parts, [&](int r) {  // C2: every range to its place in out
+        HostCtx &h = **lease[(size_t)r];
+        if (hipSetDevice(h.device) != hipSuccess ||
+            hipMemcpyAsync(out + at[(size_t)r], h.c->d_b, len[(size_t)r], hipMemcpyDeviceToHost, h.c->stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(h.c->stream) != hipSuccess)
+            rc[(size_t)r] = SNAPPY_AMD_ERR_DEVICE;
+    });
+    for (int r = 0; r < parts; r++)
+        if (rc[(size_t)r]) return rc[(size_t)r];
+    *out_len = at[(size_t)parts];
+    return SNAPPY_AMD_OK;
+}
+
+// Decoding over several devices: the first device copies the whole stream in
+// and builds its block index (K5p); each device then decodes a contiguous
+// block range from its part of the stream.  A range must start on an element
+// boundary and may not copy from an earlier range (streams this library
+// writes never do: their blocks are self-contained); otherwise -- elements
+// straddling a range start, or a range reporting SNAPPY_AMD_ERR_OFFSET -- the
+// first device decodes the whole stream, so every stream snappy_decompress
+// accepts is accepted here, with the same result.
+int snappy_decompress_buffer_multi(const int *devices, int ndev, const uint8_t *in, size_t n, uint8_t *out, size_t cap,
+                                   size_t *out_len)
+{
+    if (!out_len || !devices || ndev < 1 || (n && !in)) return SNAPPY_AMD_ERR_ARG;
+    *out_len = 0;
+    if (n == 0) return SNAPPY_AMD_OK;
+    uint64_t N = 0;
+    if (snappy_varint_decode(in, n, &N) == 0) return SNAPPY_AMD_ERR_HEADER;
+    if (N > cap) return SNAPPY_AMD_ERR_CAPACITY;
+    if (N && !out) return SNAPPY_AMD_ERR_ARG;
+    if (!length_plausible(N, n)) return SNAPPY_AMD_ERR_TRUNCATED;
+    const size_t units = (N + SNAPPY_AMD_BLOCK - 1) / SNAPPY_AMD_BLOCK;
+    const int parts = (int)std::max<size_t>(1, std::min<size_t>((size_t)ndev, units));
+    std::vector<std::unique_ptr<Lease>> lease((size_t)parts);
+    for (int r = 0; r < parts; r++) {
+        lease[(size_t)r].reset(new Lease(devices[r]));
+        if (lease[(size_t)r]->rc()) return lease[(size_t)r]->rc();
+    }
+    snappy_amd_ctx *c0 = (*lease[0])->c;
+    int rc;
+    if ((rc = grow(reinterpret_cast<void **>(&c0->d_a), &c0->d_a_cap, n + 16))) return rc;
+    if ((rc = grow(reinterpret_cast<void **>(&c0->d_b), &c0->d_b_cap, N + 16))) return rc;
+    if ((rc = grow(reinterpret_cast<void **>(&c0->d_idx), &c0->d_idx_cap, (units + 2) * sizeof(uint64_t)))) return rc;
+    HIP_OK(hipSetDevice(c0->device));
+    HIP_OK(hipMemcpyAsync(c0->d_a, in, n, hipMemcpyHostToDevice, c0->stream));
+    size_t got = 0;
+    if ((rc = snappy_amd_index_device(c0, c0->d_a, n, c0->d_idx, units + 1, &got))) return rc;
+    if (N == 0) return SNAPPY_AMD_OK;
+    std::vector<uint64_t> idx(units + 1);
+    HIP_OK(hipMemcpy(idx.data(), c0->d_idx, (units + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    const std::vector<Shard> sh = split_units(units, parts);
+    const uint64_t off_mask = (1ull << SNAPPY_AMD_IDX_OFFSET_BITS) - 1;
+    bool split = parts > 1;
+    for (int r = 1; r < parts && split; r++) split = (idx[sh[(size_t)r].u0] >> SNAPPY_AMD_IDX_OFFSET_BITS) == 0;
+    std::vector<int> rcs((size_t)parts, SNAPPY_AMD_OK);
+    if (split) {
+        on_threads(parts, [&](int r) {
+            HostCtx &h = **lease[(size_t)r];
+            snappy_amd_ctx *c = h.c;
+            const size_t u0 = sh[(size_t)r].u0, u1 = sh[(size_t)r].u1;
+            const size_t o0 = u0 * SNAPPY_AMD_BLOCK, m = std::min<uint64_t>(N, u1 * SNAPPY_AMD_BLOCK) - o0;
+            int e = SNAPPY_AMD_OK;
+            if (hipSetDevice(h.device) != hipSuccess) e = SNAPPY_AMD_ERR_DEVICE;
+            if (!e && r == 0) {  // the first range decodes in place from the whole stream
+                e = snappy_amd_decompress_device_ex(c, c->d_a, c->d_idx, m, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE, 0,
+                                                    N, c->d_b, 1);
+            } else if (!e) {
+                const uint64_t b0 = idx[u0] & off_mask, b1 = idx[u1] & off_mask;
+                std::vector<uint64_t> loc(u1 - u0 + 1);
+                for (size_t u = u0; u <= u1; u++) loc[u - u0] = (idx[u] & off_mask) - b0 + (idx[u] & ~off_mask);
+                if ((e = grow(reinterpret_cast<void **>(&c->d_a), &c->d_a_cap, (size_t)(b1 - b0) + 16)) ||
+                    (e = grow(reinterpret_cast<void **>(&c->d_b), &c->d_b_cap, m + 16)) ||
+                    (e = grow(reinterpret_cast<void **>(&c->d_idx), &c->d_idx_cap, loc.size() * sizeof(uint64_t)))) {
+                } else if (hipMemcpyAsync(c->d_a, in + b0, (size_t)(b1 - b0), hipMemcpyHostToDevice, c->stream) !=
+                               hipSuccess ||
+                           hipMemcpyAsync(c->d_idx, loc.data(), loc.size() * sizeof(uint64_t), hipMemcpyHostToDevice,
+                                          c->stream) != hipSuccess) {
+                    e = SNAPPY_AMD_ERR_DEVICE;
+                } else {
+                    e = snappy_amd_decompress_device_ex(c, c->d_a, c->d_idx, m, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE,
+                                                        SNAPPY_AMD_NO_PREAMBLE, N, c->d_b, 1);
+                }
+            }
+            if (!e && (hipMemcpyAsync(out + o0, c->d_b, m, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+                       hipStreamSynchronize(c->stream) != hipSuccess))
+                e = SNAPPY_AMD_ERR_DEVICE;
+            rcs[(size_t)r] = e;
+        });
+        bool again = false;
+        for (int r = 0; r < parts; r++) {
+            if (rcs[(size_t)r] == SNAPPY_AMD_ERR_OFFSET && r > 0) again = true;  // copies from an earlier range
+            else if (rcs[(size_t)r]) return rcs[(size_t)r];
+        }
+        if (!again) {
+            *out_len = (size_t)N;
+            return SNAPPY_AMD_OK;
+        }
+    }
+    // one device decodes the whole stream (ordered second pass for cross-block copies)
+    HIP_OK(hipSetDevice(c0->device));
+    if ((rc = snappy_amd_decompress_device(c0, c0->d_a, c0->d_idx, (size_t)N, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE,
+                                           c0->d_b)))
+        return rc;
+    HIP_OK(hipMemcpyAsync(out, c0->d_b, N, hipMemcpyDeviceToHost, c0->stream));
+    HIP_OK(hipStreamSynchronize(c0->stream));
+    *out_len = (size_t)N;
+    return SNAPPY_AMD_OK;
+}
+
+}  // extern "C"

@@ -1604,7 +1604,6 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     uint8_t *ob = reinterpret_cast<uint8_t *>(lds + kK4RingAt / 4);  // output ring: position x -> ob[x & M]
     constexpr uint32_t ring = kK4Ring, M = ring - 1;
     uint32_t *const map32 = lds + kK4MapAt / 4;      // the batch's element starts, 32 dwords
-    uint16_t *const map16 = reinterpret_cast<uint16_t *>(map32);
     const uint32_t lane = threadIdx.x;
     const uint64_t ix0 = offsets[u], ix1 = offsets[u + 1];
     // comp is 4-byte aligned; the stream starts `bias` bytes into it
@@ -1944,9 +1943,15 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             // the batch's element starts as a bitmap over [op, op_end): bit j of
             // dword j / 32 = an element starts at op + j (out_off < kK4MapBits, see
             // `over`); lane w < 32 keeps dword w, pass i reads dwords 2i, 2i + 1
-            map16[lane] = 0;
+            // (all three as u32 accesses, each behind a compiler barrier: one wave's
+            // LDS operations complete in issue order, so only the compiler could
+            // reorder the clear, the or and the read; lanes w and w + 32 store
+            // the same zero into dword w)
+            map32[lane & 31] = 0;
+            asm volatile("" ::: "memory");
             if (ex) __hip_atomic_fetch_or(map32 + (out_off >> 5), 1u << (out_off & 31), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+            asm volatile("" ::: "memory");
             const uint32_t bm = map32[lane & 31];
             // element k: kop = output start | literal flag (bit 31); kinfo = the
             // copy offset, or for a literal its window address (slot base + data

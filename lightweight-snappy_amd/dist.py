@@ -21,10 +21,13 @@ import torch.distributed as dist
 
 
 def shard_range(n_total: int, world: int, rank: int, unit: int) -> Tuple[int, int]:
-    """Byte range [off, off+len) of rank's shard: contiguous, unit-aligned."""
+    """Byte range [off, off+len) of rank's shard: contiguous, unit-aligned.
+    Rounded up, so rank 0 (which writes a SINGLE stream's preamble) always
+    owns the first unit when there is one; with fewer units than ranks the
+    empty shards are later ranks'."""
     units = (n_total + unit - 1) // unit
-    u0 = units * rank // world
-    u1 = units * (rank + 1) // world
+    u0 = -(-units * rank // world)
+    u1 = -(-units * (rank + 1) // world)
     off = u0 * unit
     return off, max(0, min(n_total, u1 * unit) - off)
 
@@ -33,6 +36,7 @@ BLOCK = 65536
 GiB = 1 << 30
 HBM_BYTES = 288 * 10**9  # MI355X HBM3E, 288 GB (MI355X_MICROARCH.md; the spec figure, the smaller reading)
 K2_SEG = 256              # csrc/snappy_kernels.h SNAPPY_K2_SEG
+COMPACT_BOUNCE = 256 << 20  # bench.py's in-place compaction of the C2 gather stages pieces of this size
 
 
 def max_output(n: int, unit: int) -> int:
@@ -63,7 +67,8 @@ def rank_plan(total: int, world: int, unit: int, piece_bytes: int, exchange: boo
     shard (back), the per-piece block indexes and the codec's scratch for the
     largest piece (K1r token lists + escapes, token counts, unit sizes, K2
     segment records, K4 status words).  With `exchange` (world > 1): C2's
-    padded all-gather buffer (world x payload) and the reassembled stream.
+    padded all-gather buffer (world x payload), compacted in place into the
+    reassembled stream through a 256 MiB staging buffer.
     `gather_decoded` (C3, opt-in) runs after the codec scratch and C2 buffers
     are released: every rank then also holds world x the largest shard."""
     shard = max(shard_range(total, world, r, unit)[1] for r in range(world))
@@ -85,7 +90,7 @@ def rank_plan(total: int, world: int, unit: int, piece_bytes: int, exchange: boo
     }
     if exchange and world > 1:
         plan["c2_gather_buffer"] = world * out_cap
-        plan["c2_stream"] = world * out_cap
+        plan["c2_compaction_bounce"] = COMPACT_BOUNCE
     plan["peak"] = sum(plan.values())
     if gather_decoded and world > 1:
         c3 = plan["shard_x"] + plan["payload_out"] + plan["decoded_back"] + plan["block_indexes"] + world * shard

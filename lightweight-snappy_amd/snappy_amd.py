@@ -41,6 +41,8 @@ BLOCK = 65536
 SINGLE = 0
 STREAMS = 1
 NO_PREAMBLE = 1
+OPT_SERIAL_INDEX = 1    # snappy_amd_set_option: one-wave index walk instead of K5p
+OPT_K1R_EXTRA_LDS = 2   # extra dynamic LDS bytes per K1r unit (occupancy experiments)
 
 _NAMES = {
     ERR_ARG: "bad argument",
@@ -97,6 +99,15 @@ _SIGS = {
     "snappy_amd_last_timings": (_c.c_int, [_c.c_void_p, _c.POINTER(_c.c_float), _c.POINTER(_c.c_float),
                                            _c.POINTER(_c.c_float)]),
     "snappy_amd_enable_timing": (_c.c_int, [_c.c_void_p, _c.c_int]),
+    "snappy_amd_set_option": (_c.c_int, [_c.c_void_p, _c.c_int, _c.c_int64]),
+    "snappy_amd_host_set_device": (_c.c_int, [_c.c_int]),
+    "snappy_amd_host_get_device": (_c.c_int, []),
+    "snappy_amd_host_release": (_c.c_int, []),
+    "snappy_amd_host_pool_size": (_c.c_size_t, []),
+    "snappy_compress_buffer_multi": (_c.c_int, [_c.POINTER(_c.c_int), _c.c_int, _c.c_void_p, _c.c_size_t, _c.c_void_p,
+                                                _c.POINTER(_c.c_size_t)]),
+    "snappy_decompress_buffer_multi": (_c.c_int, [_c.POINTER(_c.c_int), _c.c_int, _c.c_void_p, _c.c_size_t,
+                                                  _c.c_void_p, _c.c_size_t, _c.POINTER(_c.c_size_t)]),
     "snappy_amd_host_compress": (_c.c_int, [_c.c_void_p, _c.c_size_t, _c.c_uint64, _c.c_void_p, _c.c_size_t,
                                             _c.POINTER(_c.c_size_t)]),
     "snappy_amd_host_decompress": (_c.c_int, [_c.c_void_p, _c.c_size_t, _c.c_void_p, _c.c_size_t,
@@ -210,14 +221,48 @@ def uncompressed_length(data) -> int:
     return v.value
 
 
+def _declared_length(data, n: int) -> int:
+    """The preamble's N, refused (as the library refuses it) when n bytes of
+    stream cannot expand to it: at most 64 output bytes per 3-byte element."""
+    N = uncompressed_length(data)
+    if N // 22 > n:
+        raise SnappyError(ERR_TRUNCATED, "decompress")
+    return N
+
+
 def decompress(data) -> bytes:
     p, n, keep = _buf(data)
     if n == 0:
         return b""
-    N = uncompressed_length(data)
+    N = _declared_length(data, n)
     out = ctypes.create_string_buffer(max(N, 1))
     got = ctypes.c_size_t(0)
     _check(lib().snappy_decompress_buffer(p, n, out, N, ctypes.byref(got)), "decompress")
+    return out.raw[: got.value]
+
+
+def compress_multi(data, devices) -> bytes:
+    """snappy_compress_buffer_multi: one stream (== compress(data)) made on
+    several devices, each compressing a contiguous range of blocks."""
+    p, n, keep = _buf(data)
+    devs = (ctypes.c_int * len(devices))(*devices)
+    out = ctypes.create_string_buffer(max(max_compressed_length(n), 1))
+    got = ctypes.c_size_t(0)
+    _check(lib().snappy_compress_buffer_multi(devs, len(devices), p, n, out, ctypes.byref(got)), "compress_multi")
+    return out.raw[: got.value]
+
+
+def decompress_multi(data, devices) -> bytes:
+    """snappy_decompress_buffer_multi: decompress(data) over several devices."""
+    p, n, keep = _buf(data)
+    if n == 0:
+        return b""
+    N = _declared_length(data, n)
+    devs = (ctypes.c_int * len(devices))(*devices)
+    out = ctypes.create_string_buffer(max(N, 1))
+    got = ctypes.c_size_t(0)
+    _check(lib().snappy_decompress_buffer_multi(devs, len(devices), p, n, out, N, ctypes.byref(got)),
+           "decompress_multi")
     return out.raw[: got.value]
 
 
@@ -240,7 +285,7 @@ def decompress_indexed(data, index_file: bytes) -> bytes:
         return b""
     _, ent = read_index(index_file)
     arr = (ctypes.c_uint64 * max(len(ent), 1))(*ent)
-    N = uncompressed_length(data)
+    N = _declared_length(data, n)
     out = ctypes.create_string_buffer(max(N, 1))
     got = ctypes.c_size_t(0)
     _check(lib().snappy_amd_host_decompress_idx(p, n, arr, len(ent), out, N, ctypes.byref(got)), "decompress_indexed")
@@ -297,6 +342,11 @@ class Codec:
     def trim(self) -> None:
         """Free the context's scratch (the next call allocates it again)."""
         _check(lib().snappy_amd_trim(self._h), "trim")
+
+    def set_option(self, option: int, value: int) -> None:
+        """snappy_amd_set_option: OPT_SERIAL_INDEX (1: one-wave index walk),
+        OPT_K1R_EXTRA_LDS (extra dynamic LDS bytes per K1r unit)."""
+        _check(lib().snappy_amd_set_option(self._h, option, value), "set_option")
 
     def enable_timing(self, on: bool = True) -> None:
         _check(lib().snappy_amd_enable_timing(self._h, 1 if on else 0), "enable_timing")

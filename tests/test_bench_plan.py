@@ -18,7 +18,13 @@ GiB = 1 << 30
 
 def test_default_sizes():
     a = bench.parse([])
-    assert bench.resolve_sizes(a, 1, 0) == (False, GiB, 0, GiB, GiB)  # configs[1]
+    # configs[3] at every N: the N = 1 point is the same 64 GiB job (one curve)
+    assert bench.resolve_sizes(a, 1, 0) == (True, 64 * GiB, 0, 64 * GiB, 64 * GiB)
+    a1 = bench.parse(["--bytes-per-gpu", str(GiB)])  # configs[1] alone
+    assert bench.resolve_sizes(a1, 1, 0) == (False, GiB, 0, GiB, GiB)
+    a2 = bench.parse(["--workload", "text64k"])  # another workload alone at N = 1: 1 GiB
+    assert bench.resolve_sizes(a2, 1, 0) == (False, GiB, 0, GiB, GiB)
+    assert bench.resolve_sizes(a2, 2, 1)[:2] == (True, 64 * GiB)
     for world in (2, 4, 8):  # configs[3]: 64 GiB strong-scaled
         strong, total, off, n, n_max = bench.resolve_sizes(a, world, world - 1)
         assert strong and total == 64 * GiB and n == n_max == 64 * GiB // world

@@ -67,7 +67,8 @@ def _worker(rank, world, port, n, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n", [(2, 5 * BLOCK + 123), (2, 4 * BLOCK), (3, 7 * BLOCK + 1)])
+@pytest.mark.parametrize("world,n", [(2, 5 * BLOCK + 123), (2, 4 * BLOCK), (3, 7 * BLOCK + 1),
+                                     (8, 21 * BLOCK + 77), (8, 5 * BLOCK)])
 def test_sharded_stream_identical(world, n):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -211,6 +212,25 @@ def test_bench_memory_within_plan(world):
     assert 0 < m["rank_peak_bytes"] <= m["planned_peak_bytes_per_rank"], m
     # the plan is a worst-case bound, not a vacuous one: text uses a good part of it
     assert m["rank_peak_bytes"] >= 0.3 * m["planned_peak_bytes_per_rank"], m
+
+
+@pytest.mark.gpu
+def test_bench_world8_rehearsal():
+    """configs[3]'s 8-rank path on the one GPU of a box: bench.py --gpus 8
+    spawns 8 ranks (torch.distributed.run, gloo collectives, all ranks on
+    cuda:0) of a 256 MiB strong-scaled job in 16 MiB pieces -- C1 in every
+    step, the end-to-end loop with the C2 gather compacted in place into the
+    stream, per-shard checksums and the round trip verified on every rank,
+    and every rank's measured peak within dist.rank_plan for that size."""
+    total = 256 << 20
+    d = _bench("--gpus", "8", "--dist-backend", "gloo", "--total-bytes", str(total), "--piece-bytes", str(16 << 20),
+               "--steps", "1", "--warmup", "1", "--no-host-e2e")
+    assert d["n_gpus"] == 8 and d["scaling"] == "strong" and d["round_trip_ok"]
+    assert d["config"]["total_bytes"] == total and d["config"]["bytes_per_gpu"] == total // 8
+    assert d["config"]["pieces_per_gpu"] == 2
+    assert d["exchange"]["verified"] and d["value_end_to_end"] > 0
+    m = d["memory"]
+    assert 0 < m["rank_peak_bytes"] <= m["planned_peak_bytes_per_rank"], m
 
 
 @pytest.mark.gpu

@@ -167,6 +167,40 @@ def test_cli_streaming_multi_chunk():
         assert open(dec, "rb").read() == data
 
 
+DROPIN = os.path.join(ROOT, "oracle", "_ref", "snappy_dropin")
+
+
+@pytest.mark.skipif(not os.path.exists(DROPIN), reason="oracle/_ref/snappy_dropin is built by build() where "
+                                                       "/root/reference exists and travels with the tree")
+def test_reference_cli_dropin(golden):
+    """The reference's own src/cmd.c (with IO_utils.c and result.c), unchanged,
+    linked against libsnappy_amd.so (oracle/Makefile `snappy_dropin`) and run
+    on the GPU: -c of configs[0]'s 1,000,000-byte text gives the reference's
+    golden bytes, -d restores it; the 150 MiB mixed file (three 64 MiB
+    pipeline chunks) comes out equal to the one-shot reference stream and
+    round-trips.  src/cmd.c:86-98 calls snappy_compress / snappy_decompress."""
+    e = next(x for x in golden["entries"] if x["name"] == "text_1000000")
+    one = make_input(e["spec"])
+    mixed = np.concatenate([datagen.make("T", 70 << 20, 41), datagen.make("R", 30 << 20, 42),
+                            np.zeros(10 << 20, np.uint8), datagen.make("T", (40 << 20) + 12345, 43)]).tobytes()
+    with tempfile.TemporaryDirectory() as d:
+        for name, data, want_sha in (("text_1000000", one, e["out_sha256"]), ("mixed_150MiB", mixed, None)):
+            src, snp, dec = (os.path.join(d, f"{name}{x}") for x in ("", ".snp", ".dec"))
+            open(src, "wb").write(data)
+            r = subprocess.run([DROPIN, "-c", "-r", src, snp], capture_output=True, text=True, timeout=120)
+            assert r.returncode == 0, r.stderr
+            assert "MB/s" in r.stdout  # src/result.c's report: the reference CLI ran to its end
+            got = open(snp, "rb").read()
+            if want_sha:
+                assert sha(got) == want_sha, name
+            else:
+                assert got == oracle.compress(data), name
+            r = subprocess.run([DROPIN, "-d", "-r", snp, dec], capture_output=True, text=True, timeout=120)
+            assert r.returncode == 0, r.stderr
+            assert open(dec, "rb").read() == data, name
+            progress(f"dropin {name}: ok")
+
+
 def test_full_size_streams_1gib(codec):
     """BASELINE.json configs[1] at full size: 1 GiB of 32 KiB text streams,
     bit-exact against the (threaded) oracle and round-tripped on the GPU."""
@@ -273,15 +307,14 @@ def _index_both(codec, d):
     """(code, n, offsets) from the chunk-parallel K5p and from the serial K5."""
     res = []
     for serial in (False, True):
-        if serial:
-            os.environ["SNAPPY_AMD_K5_SERIAL"] = "1"
+        codec.set_option(snappy_amd.OPT_SERIAL_INDEX, int(serial))
         try:
             n, offs = codec.index_tensor(d)
             res.append((0, n, offs.cpu().numpy().copy()))
         except snappy_amd.SnappyError as e:
             res.append((e.code, None, None))
         finally:
-            os.environ.pop("SNAPPY_AMD_K5_SERIAL", None)
+            codec.set_option(snappy_amd.OPT_SERIAL_INDEX, 0)
     return res
 
 
@@ -844,3 +877,143 @@ def test_file_api_mapped_output_error_leaves_file():
                     assert open(dec, "rb").read() == prefix, (mm, seek)
             finally:
                 os.environ.pop("SNAPPY_AMD_NO_MMAP", None)
+
+
+def test_host_api_concurrent_threads():
+    """Reentrancy: four threads compress and decompress different
+    inputs through the host-buffer API at once, and two threads run the FILE*
+    pipelines on two files at once; each call leases its own pooled host
+    context, every output equals the oracle's, and the pool keeps the idle
+    contexts (at least one per concurrent caller) until released."""
+    import ctypes
+    import threading
+    lib = snappy_amd.lib()
+    lib.snappy_amd_host_release()
+    inputs = [datagen.make(k, n, s).tobytes() for k, n, s in
+              (("T", (24 << 20) + 7, 61), ("R", 9 << 20, 62), ("T", 40 << 20, 63), ("P", 17 << 20, 64))]
+    wants = [oracle.compress(x) for x in inputs]
+    errs = []
+    start = threading.Barrier(len(inputs))
+
+    def work(i):
+        try:
+            start.wait()
+            for _ in range(3):
+                c = snappy_amd.compress(inputs[i])
+                assert c == wants[i], i
+                assert snappy_amd.decompress(c) == inputs[i], i
+        except Exception as e:  # noqa: BLE001
+            errs.append((i, repr(e)))
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(inputs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    assert lib.snappy_amd_host_pool_size() >= 2
+    # the FILE* pipelines, two files at once
+    libc = ctypes.CDLL(None)
+    libc.fopen.restype = ctypes.c_void_p
+    libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    libc.fclose.argtypes = [ctypes.c_void_p]
+    files = [inputs[2] + inputs[0], inputs[1] * 12]  # 64 MiB+ (two chunks) and 108 MiB
+    with tempfile.TemporaryDirectory(dir="/dev/shm" if os.path.isdir("/dev/shm") else None) as d:
+        def file_work(i):
+            try:
+                src, snp, dec = (os.path.join(d, f"{i}{x}").encode() for x in ("", ".snp", ".dec"))
+                open(src, "wb").write(files[i])
+                start2.wait()
+                fi, fo = libc.fopen(src, b"rb"), libc.fopen(snp, b"wb")
+                lib.snappy_compress(ctypes.c_void_p(fi), ctypes.c_ulonglong(len(files[i])), ctypes.c_void_p(fo))
+                assert lib.snappy_amd_last_status() == 0
+                libc.fclose(ctypes.c_void_p(fi)), libc.fclose(ctypes.c_void_p(fo))
+                fi, fo = libc.fopen(snp, b"rb"), libc.fopen(dec, b"wb")
+                assert lib.snappy_decompress(ctypes.c_void_p(fi), ctypes.c_void_p(fo)) == 0
+                libc.fclose(ctypes.c_void_p(fi)), libc.fclose(ctypes.c_void_p(fo))
+                assert open(snp, "rb").read() == oracle.compress(files[i]), i
+                assert open(dec, "rb").read() == files[i], i
+            except Exception as e:  # noqa: BLE001
+                errs.append(("file", i, repr(e)))
+
+        start2 = threading.Barrier(2)
+        th = [threading.Thread(target=file_work, args=(i,)) for i in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    assert not errs, errs
+    assert lib.snappy_amd_host_release() == 0 and lib.snappy_amd_host_pool_size() == 0
+
+
+def test_host_device_selection():
+    lib = snappy_amd.lib()
+    assert lib.snappy_amd_host_set_device(0) == 0 and lib.snappy_amd_host_get_device() == 0
+    assert lib.snappy_amd_host_set_device(4096) == snappy_amd.ERR_DEVICE
+    assert lib.snappy_amd_host_set_device(-1) == 0
+
+
+def test_multi_device_buffer_api(golden):
+    """snappy_compress_buffer_multi / snappy_decompress_buffer_multi with the
+    one device of the box listed 1-3 times (a context and a thread each): the
+    stream equals the one-device stream (the reference's bytes), the decode
+    splits into block ranges; streams whose ranges are not self-contained
+    (the reference-decodable cross-block vectors) still decode exactly."""
+    for kind, n, seed in (("T", (9 << 20) + 12345, 71), ("R", 3 << 20, 72), ("T", 65536 * 2, 73), ("T", 100, 74)):
+        data = datagen.make(kind, n, seed).tobytes()
+        want = oracle.compress(data)
+        for devs in ([0], [0, 0], [0, 0, 0]):
+            got = snappy_amd.compress_multi(data, devs)
+            assert got == want, (kind, n, devs)
+            assert snappy_amd.decompress_multi(got, devs) == data, (kind, n, devs)
+    assert snappy_amd.compress_multi(b"", [0, 0]) == b""
+    for v in golden["xblock_vectors"]:
+        stream = _xblock_stream(v)
+        out = snappy_amd.decompress_multi(stream, [0, 0, 0])
+        assert len(out) == v["out_len"] and sha(out) == v["out_sha256"], v["name"]
+    with pytest.raises(snappy_amd.SnappyError):
+        snappy_amd.decompress_multi(want[:-3], [0, 0])
+
+
+def test_decompress_file_bogus_length():
+    """A preamble declaring more than the stream could ever produce (10 bytes
+    claiming 2^40) is refused before any output is mapped or preallocated: the
+    output file keeps its size and its allocated blocks.  A plausible length
+    over a corrupt body fails in the decoder, and the blocks preallocated for
+    it past the file's end are released (st_blocks back to the old value)."""
+    import ctypes
+    libc = ctypes.CDLL(None)
+    libc.fopen.restype = ctypes.c_void_p
+    libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    libc.fclose.argtypes = [ctypes.c_void_p]
+    lib = snappy_amd.lib()
+    rng = np.random.default_rng(12)
+    bogus = snappy_amd.varint_encode(1 << 40) + b"\x00abc"
+    corrupt = snappy_amd.varint_encode(80 << 20) + bytes([0x01]) + rng.integers(0, 256, 4 << 20, np.uint8).tobytes()
+    prefix = b"KEEP" * 1024
+    with tempfile.TemporaryDirectory(dir="/dev/shm" if os.path.isdir("/dev/shm") else None) as d:
+        for name, stream, want in (("bogus", bogus, snappy_amd.ERR_TRUNCATED), ("corrupt", corrupt, None)):
+            src, dec = os.path.join(d, name), os.path.join(d, name + ".out")
+            open(src, "wb").write(stream)
+            for mm in ("1", None):
+                if mm:
+                    os.environ["SNAPPY_AMD_NO_MMAP"] = mm
+                try:
+                    open(dec, "wb").write(prefix)
+                    before = os.stat(dec)
+                    fi, fo = libc.fopen(src.encode(), b"rb"), libc.fopen(dec.encode(), b"ab")
+                    rc = lib.snappy_decompress(ctypes.c_void_p(fi), ctypes.c_void_p(fo))
+                    libc.fclose(ctypes.c_void_p(fi)), libc.fclose(ctypes.c_void_p(fo))
+                    assert rc != 0 and (want is None or rc == want), (name, mm, rc)
+                    fi, fo = libc.fopen(src.encode(), b"rb"), libc.fopen(dec.encode(), b"r+b")
+                    rc = lib.snappy_decompress(ctypes.c_void_p(fi), ctypes.c_void_p(fo))
+                    libc.fclose(ctypes.c_void_p(fi)), libc.fclose(ctypes.c_void_p(fo))
+                    assert rc != 0 and (want is None or rc == want), (name, mm, rc)
+                    after = os.stat(dec)
+                    assert after.st_size == before.st_size and open(dec, "rb").read() == prefix, (name, mm)
+                    assert after.st_blocks <= before.st_blocks, (name, mm, before.st_blocks, after.st_blocks)
+                finally:
+                    os.environ.pop("SNAPPY_AMD_NO_MMAP", None)
+    with pytest.raises(snappy_amd.SnappyError) as ei:
+        snappy_amd.decompress(bogus)
+    assert ei.value.code == snappy_amd.ERR_TRUNCATED

@@ -13,6 +13,8 @@ layout = snappy_amd.SINGLE if chunk == 65536 else snappy_amd.STREAMS
 a = datagen.make(kind, n, 1234 if kind == "T" else 1)
 x = torch.from_numpy(a).cuda()
 c = snappy_amd.Codec(0)
+if os.environ.get("SNAPPY_K1R_DYNLDS"):  # occupancy experiments: extra dynamic LDS per unit
+    c.set_option(snappy_amd.OPT_K1R_EXTRA_LDS, int(os.environ["SNAPPY_K1R_DYNLDS"]))
 comp, offs = c.compress_tensor(x, chunk=chunk, layout=layout)
 comp, offs = c.compress_tensor(x, chunk=chunk, layout=layout)
 torch.cuda.synchronize()

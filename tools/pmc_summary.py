@@ -52,7 +52,9 @@ for w in sorted(os.listdir(src)):
     write = per_kernel(os.path.join(d, "write", "run_counter_collection.csv"))
     sq = per_kernel(os.path.join(d, "sq", "run_counter_collection.csv"))
     n = line["config"]["bytes_per_gpu"]
-    res = {"workload": w, "bytes_per_gpu": n, "round": rnd,
+    # bench.py matches a summary to its line by workload and launch size
+    res = {"label": w, "workload": line["config"].get("workload_name", w), "bytes_per_gpu": n,
+           "launch_bytes": line["config"].get("launch_bytes", n), "round": rnd,
            "note": "per launch; FETCH_SIZE KiB x1024 x2 (gfx950 half-count correction), WRITE_SIZE KiB x1024; "
                    "SQ_* as rocprofv3 reports them (SQ_WAVE_CYCLES/SQ_BUSY_CYCLES in quad-cycles per the guide)",
            "kernels": {}}

@@ -1,7 +1,9 @@
 #!/bin/bash
 # Round profiling recipe (run on the GPU box from the repo root):
-#   tools/profile_round.sh [workload ...]      (default: every bench workload)
-# For each workload W, under gpurun_out/prof/W/:
+#   tools/profile_round.sh [label ...]      (default: every bench workload)
+# Labels: config3 (the default bench job: 64 GiB of 32 KiB text streams, 8 GiB
+# launches), text32k (configs[1], 1 GiB), text64k, random, repeat, decode10g.
+# For each label W, under gpurun_out/prof/W/:
 #   bench.json    the bench.py line (CPU baselines on a bounded sample)
 #   trace/        rocprofv3 --kernel-trace --stats of the same command
 #   fetch/ write/ rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE (separate passes, kernel trace only)
@@ -11,16 +13,22 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-WLS=${*:-"text32k text64k random repeat decode10g"}
+WLS=${*:-"config3 text32k text64k random repeat decode10g"}
 STEPS=${STEPS:-5}
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"
 run() {  # workload
     # --no-sub: the profiled process runs this workload only (the default line also runs the
     # other configs, whose launches of the same kernels would be averaged into W's counters)
-    local w=$1 d=gpurun_out/prof/$1 q="--workload $1 --no-cpu-baseline --no-host-e2e --no-sub"
+    local w=$1 d=gpurun_out/prof/$1 sel
+    case $w in
+        config3) sel="--workload text32k" ;;
+        text32k) sel="--workload text32k --bytes-per-gpu 1073741824" ;;
+        *) sel="--workload $w" ;;
+    esac
+    local q="$sel --no-cpu-baseline --no-host-e2e --no-sub"
     mkdir -p $d &&
     echo "[$(date +%T)] $w: bench" &&
-    timeout -k 10 400 python3 bench.py --workload $w --steps $STEPS --warmup 2 --cpu-sample-bytes 268435456 --no-sub \
+    timeout -k 10 400 python3 bench.py $sel --steps $STEPS --warmup 2 --cpu-sample-bytes 268435456 --no-sub \
         > $d/bench.json 2> $d/bench.err &&
     echo "[$(date +%T)] $w: kernel trace" &&
     timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $d/trace -o run --output-format csv -- \

@@ -803,11 +803,15 @@ int dec_stage_init(DecStage &d)
 // own streams, scratch and pinned staging.  The pool's lock is held only to
 // take or return a context.  The device is the calling thread's
 // (snappy_amd_host_set_device), else SNAPPY_AMD_DEVICE (read once), else 0.
+constexpr int kPipeLanes = 4;                    // host-buffer compress: chunks in flight
+constexpr size_t kPipeChunk = (size_t)64 << 20;  // ... of this many bytes (1,024 blocks)
+
 struct HostCtx {
     int device = 0;
-    snappy_amd_ctx *c = nullptr;  // host-buffer path and the FILE* decoder
-    StreamSlot slots[2];          // the FILE* compressor's two pipeline slots
-    DecStage dec;                 // the FILE* decoder's pinned staging
+    snappy_amd_ctx *c = nullptr;           // host-buffer path and the FILE* decoder
+    StreamSlot slots[2];                   // the FILE* compressor's two pipeline slots
+    DecStage dec;                          // the FILE* decoder's pinned staging
+    snappy_amd_ctx *pipe[kPipeLanes] = {}; // the host-buffer compressor's chunk lanes
 };
 
 void host_free(HostCtx *h)
@@ -815,6 +819,7 @@ void host_free(HostCtx *h)
     if (!h) return;
     (void)hipSetDevice(h->device);
     for (auto &s : h->slots) slot_free(s);
+    for (auto *p : h->pipe) snappy_amd_destroy(p);
     dec_stage_free(h->dec);
     snappy_amd_destroy(h->c);
     delete h;
@@ -935,6 +940,58 @@ size_t snappy_amd_host_pool_size(void)
     return g_pool.size();
 }
 
+// A host buffer of more than one 64 MiB chunk: each chunk (a multiple of the
+// 65,536-byte block, so the bytes are those of the one-shot stream; chunks
+// after the first without the preamble) goes to one of kPipeLanes contexts of
+// its own stream -- H2D, K1r/K3/K2, the compressed size back to pinned memory
+// -- so the chunks' copies and kernels overlap and their kernels fill the chip
+// together (one 64 MiB chunk is 1,024 blocks on 3,072 wave slots); the
+// compressed chunks come back in order, each to the offset its predecessors'
+// sizes give.  A lane is reused once its previous chunk has come back.
+int host_compress_pipelined(HostCtx &h, const uint8_t *in, size_t n, uint64_t header_value, uint8_t *out,
+                            size_t cap, size_t *out_len)
+{
+    const size_t nch = (n + kPipeChunk - 1) / kPipeChunk;
+    const int lanes = (int)std::min<size_t>((size_t)kPipeLanes, nch);
+    int rc;
+    for (int i = 0; i < lanes; i++)
+        if (!h.pipe[i] && (rc = snappy_amd_create(h.device, &h.pipe[i]))) {
+            h.pipe[i] = nullptr;
+            return rc;
+        }
+    size_t off = 0;  // compressed bytes placed so far
+    auto drain = [&](size_t k) -> int {
+        snappy_amd_ctx *c = h.pipe[k % (size_t)lanes];
+        HIP_OK(hipStreamSynchronize(c->stream));
+        const size_t len = (size_t)*c->h_total;
+        if (off + len > cap) return SNAPPY_AMD_ERR_CAPACITY;
+        HIP_OK(hipMemcpyAsync(out + off, c->d_b, len, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipStreamSynchronize(c->stream));
+        off += len;
+        return SNAPPY_AMD_OK;
+    };
+    for (size_t k = 0; k < nch; k++) {
+        if (k >= (size_t)lanes && (rc = drain(k - (size_t)lanes))) return rc;
+        snappy_amd_ctx *c = h.pipe[k % (size_t)lanes];
+        const size_t m = std::min(kPipeChunk, n - k * kPipeChunk);
+        const size_t units = (m + SNAPPY_AMD_BLOCK - 1) / SNAPPY_AMD_BLOCK;
+        if ((rc = grow(reinterpret_cast<void **>(&c->d_a), &c->d_a_cap, m + 16)) ||
+            (rc = grow(reinterpret_cast<void **>(&c->d_b), &c->d_b_cap,
+                       snappy_amd_max_output(m, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE))) ||
+            (rc = grow(reinterpret_cast<void **>(&c->d_idx), &c->d_idx_cap, (units + 1) * sizeof(uint64_t))))
+            return rc;
+        HIP_OK(hipMemcpyAsync(c->d_a, in + k * kPipeChunk, m, hipMemcpyHostToDevice, c->stream));
+        if ((rc = compress_impl(c, c->d_a, m, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE, k ? SNAPPY_AMD_NO_PREAMBLE : 0,
+                                header_value, c->d_b, c->d_idx, nullptr)))
+            return rc;
+        HIP_OK(hipMemcpyAsync(c->h_total, c->total, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    }
+    for (size_t k = nch > (size_t)lanes ? nch - (size_t)lanes : 0; k < nch; k++)
+        if ((rc = drain(k))) return rc;
+    *out_len = off;
+    return SNAPPY_AMD_OK;
+}
+
 int snappy_amd_host_compress(const uint8_t *in, size_t n, uint64_t header_value, uint8_t *out, size_t cap,
                              size_t *out_len)
 {
@@ -943,6 +1000,7 @@ int snappy_amd_host_compress(const uint8_t *in, size_t n, uint64_t header_value,
     if (n == 0) return SNAPPY_AMD_OK;
     Lease h(host_device());
     if (h.rc()) return h.rc();
+    if (n > kPipeChunk) return host_compress_pipelined(*h, in, n, header_value, out, cap, out_len);
     size_t len = 0;
     int rc = host_compress_stage(*h, in, n, 0, header_value, &len);
     if (rc) return rc;

@@ -698,6 +698,518 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     const uint64_t t_loop = clock64();
     uint32_t n_probe = 0, n_match = 0, n_round = 0, n_refresh = 0;
 #endif
+
+    // ---- k1r_asm_rounds: the lane-space round of the C++ loop below (32 KiB
+    // units), hand-scheduled as one loop: drain the deferred token, hit ballot,
+    // first hit f and its candidate c, the 64 bytes at pf = q0 + f and at c
+    // gathered (ds_bpermute; c's registers by s_set_gpr_idx), the inserts of
+    // lanes lo0..f (lane-ordered, highest lane wins a slot), the next round's
+    // entries read while the verification runs, the match length from the
+    // first differing byte; a round without a hit inserts its nk probes.  It
+    // leaves the loop with `code`: 1 = skip past the step-1 range or
+    // is_block_end, 2 = the window must move (refresh), 3 = the next round's
+    // probes reach a step of 2 (skip > 64 - DMAX: the C++ round), and mid-round
+    // (inserts done, entries read) 4 = 64 or more equal bytes (C++ extends the
+    // match), 5 = a tag collision (C++ finishes the miss).  Everything the
+    // compiler schedules around it -- waits, DPP, cross-lane reads -- is
+    // written out with its wait states: a VALU-written SGPR or VCC is read by
+    // VALU two states later (v_cndmask, v_readlane sources); LDS results are
+    // waited for by count (pa, ca before the two entry reads); it exits with
+    // lgkmcnt(0), so `ent`/`ent_t` are complete when the compiler reads them.
+    // m0 (the writelane lane select) is saved and restored.  The loop always
+    // advances p (a match by >= 4, a missing round by nk >= 1), so it ends.
+#if !defined(SNAPPY_K1R_STATS) && !defined(SNAPPY_K1R_LSTAMPS) && !defined(SNAPPY_K1R_CXX_ROUNDS) && \
+    !defined(SNAPPY_K1R_PACKED3)
+#define K1R_ASM_ROUNDS 1
+#ifndef SNAPPY_K1R_ASM_V
+#define SNAPPY_K1R_ASM_V 2
+#endif
+#else
+#define K1R_ASM_ROUNDS 0
+#endif
+#if SNAPPY_K1R_ASM_V == 1
+#define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32)                                                  \
+    do {                                                                                            \
+        uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4;                           \
+        uint64_t _valid, _hm;                                                                       \
+        asm volatile(                                                                               \
+            "s_mov_b32 %[m0s], m0\n"                                                                \
+            "L%=_top:\n\t"                                                                          \
+            "s_mov_b32 m0, %[pend]\n\t"                                                             \
+            "v_writelane_b32 %[tka], %[dka], m0\n\t"                                                \
+            "v_writelane_b32 %[tkb], %[dkb], m0\n\t"                                                \
+            "s_add_u32 %[pend], %[pend], %[dkn]\n\t"                                                \
+            "s_mov_b32 %[dkn], 0\n\t"                                                               \
+            "s_cmp_gt_u32 %[skip], %[skipmax]\n\t"                                                  \
+            "s_cbranch_scc1 L%=_x3\n\t"                                                             \
+            "s_lshl_b64 %[valid], %[dmask], %[lane0]\n\t"                                           \
+            "s_and_b64 %[valid], %[valid], %[mwin]\n\t"                                             \
+            "v_cmp_gt_i32_e32 vcc, %[lane0], %[pdl1]\n\t" /* vcc = not in-round */                  \
+            "s_waitcnt lgkmcnt(0)\n\t"                                                              \
+            "v_xor_b32_sdwa %[t0], %[entt], %[word] dst_sel:DWORD dst_unused:UNUSED_PAD "            \
+            "src0_sel:DWORD src1_sel:WORD_1\n\t"                                                    \
+            "s_nop 0\n\t"                                                                           \
+            "v_cndmask_b32_sdwa %[t0], %[pdnz], %[t0], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "     \
+            "src0_sel:DWORD src1_sel:BYTE_0\n\t"                                                    \
+            "v_cmp_eq_u32_e64 %[hm], 0, %[t0]\n\t"                                                  \
+            "s_and_b64 %[hm], %[hm], %[valid]\n\t"                                                  \
+            "s_cmp_eq_u64 %[hm], 0\n\t"                                                             \
+            "s_cbranch_scc1 L%=_nohit\n\t"                                                          \
+            "s_ff1_i32_b64 %[f], %[hm]\n\t"                                                         \
+            "v_cndmask_b32_sdwa %[t1], %[pdc], %[ent], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "     \
+            "src0_sel:DWORD src1_sel:WORD_0\n\t"                                                    \
+            "s_add_u32 %[pf], %[q0], %[f]\n\t"                                                      \
+            "s_and_b32 %[s0], %[pf], -4\n\t"                                                        \
+            "v_add_u32_e32 %[t2], %[s0], %[lane4]\n\t"                                              \
+            "ds_bpermute_b32 %[t2], %[t2], %[dv]\n\t" /* pa: dwords at pf */                        \
+            "s_nop 1\n\t"                                                                           \
+            "v_readlane_b32 %[c], %[t1], %[f]\n\t"                                                  \
+            "s_and_b32 %[c], %[c], 0xffff\n\t"                                                      \
+            "s_lshr_b32 %[s0], %[c], 8\n\t"                                                         \
+            "s_bfe_u32 %[s1], %[c], 0x60002\n\t"                                                    \
+            "s_set_gpr_idx_on %[s0], gpr_idx(SRC0)\n\t"                                             \
+            "v_mov_b32_e32 %[t3], v2\n\t"                                                           \
+            "v_mov_b32_e32 %[t4], v3\n\t"                                                           \
+            "s_set_gpr_idx_off\n\t"                                                                 \
+            "v_cmp_gt_u32_e32 vcc, %[s1], %[lane]\n\t" /* lane < l0: register R + 1 */              \
+            "s_and_b32 %[s0], %[c], -4\n\t"                                                         \
+            "v_add_u32_e32 %[t1], %[s0], %[lane4]\n\t"                                              \
+            "s_nop 0\n\t"                                                                           \
+            "v_cndmask_b32_e32 %[t3], %[t3], %[t4], vcc\n\t"                                        \
+            "ds_bpermute_b32 %[t3], %[t1], %[t3]\n\t" /* ca: dwords at c */                         \
+            "s_add_i32 %[s0], %[lane0], -1\n\t"                                                     \
+            "s_cmp_lt_u32 %[lane0], %[f]\n\t"                                                       \
+            "s_cselect_b32 %[s0], %[s0], %[lane0]\n\t" /* lo0 */                                    \
+            "v_subrev_u32_e32 %[t4], %[s0], %[lane]\n\t"                                            \
+            "s_sub_u32 %[s0], %[f], %[s0]\n\t"                                                      \
+            "v_cmp_ge_u32_e32 vcc, %[s0], %[t4]\n\t" /* lanes lo0 .. f insert */                    \
+            "s_and_b32 %[s2], %[pf], 3\n\t"                                                         \
+            "s_mul_i32 %[s2], %[s2], 0xfefefeff\n\t"                                                \
+            "v_cndmask_b32_e32 %[t4], %[dummy], %[adr], vcc\n\t"                                    \
+            "ds_write_b16 %[t4], %[word]\n\t"                                                       \
+            "v_lshrrev_b32_e32 %[t4], 1, %[t4]\n\t"                                                 \
+            "ds_write_b8_d16_hi %[t4], %[word] offset:%[tagb]\n\t"                                  \
+            "ds_read_u16 %[ent], %[adr]\n\t"                                                        \
+            "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"                                        \
+            "s_add_i32 %[s2], %[s2], 0x7060504\n\t"                                                 \
+            "s_and_b32 %[s3], %[c], 3\n\t"                                                          \
+            "s_mul_i32 %[s3], %[s3], 0xfefefeff\n\t"                                                \
+            "s_add_i32 %[s3], %[s3], 0x7060504\n\t"                                                 \
+            "s_waitcnt lgkmcnt(2)\n\t" /* pa, ca and the inserts; the entry reads stay in flight */ \
+            "v_mov_b32_dpp %[t1], %[t2] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
+            "v_mov_b32_dpp %[t4], %[t3] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
+            "v_perm_b32 %[t2], %[t2], %[t1], %[s2]\n\t"                                             \
+            "v_perm_b32 %[t3], %[t3], %[t4], %[s3]\n\t"                                             \
+            "v_cmp_ne_u32_e32 vcc, %[t2], %[t3]\n\t"                                                \
+            "v_xor_b32_e32 %[t2], %[t2], %[t3]\n\t"                                                 \
+            "v_or_b32_e32 %[t2], 1, %[t2]\n\t"                                                      \
+            "v_ffbh_u32_e32 %[t2], %[t2]\n\t"                                                       \
+            "v_lshrrev_b32_e32 %[t2], 3, %[t2]\n\t"                                                 \
+            "v_or_b32_e32 %[t2], %[t2], %[lane4]\n\t" /* the prefix length if this dword differs */ \
+            "s_and_b32 %[s1], vcc_lo, 0xffff\n\t"                                                   \
+            "s_cmp_eq_u32 %[s1], 0\n\t"                                                             \
+            "s_cbranch_scc1 L%=_x4\n\t"                                                             \
+            "s_ff1_i32_b32 %[s1], %[s1]\n\t"                                                        \
+            "s_nop 1\n\t"                                                                           \
+            "v_readlane_b32 %[s0], %[t2], %[s1]\n\t"                                                \
+            "s_sub_u32 %[s1], %[L], %[pf]\n\t"                                                      \
+            "s_min_u32 %[s0], %[s0], %[s1]\n\t"                                                     \
+            "s_cmp_lt_u32 %[s0], 4\n\t"                                                             \
+            "s_cbranch_scc1 L%=_x5\n\t"                                                             \
+            "s_lshl_b32 %[s1], %[s0], 16\n\t"                                                       \
+            "s_or_b32 %[dka], %[s1], %[pf]\n\t"                                                     \
+            "s_sub_u32 %[dkb], %[pf], %[c]\n\t"                                                     \
+            "s_mov_b32 %[dkn], 1\n\t"                                                               \
+            "s_add_u32 %[p], %[pf], %[s0]\n\t"                                                      \
+            "s_mov_b32 %[skip], 32\n\t"                                                             \
+            "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                        \
+            "s_cbranch_scc1 L%=_x1\n\t"                                                             \
+            "s_sub_u32 %[lane0], %[p], %[q0]\n\t"                                                   \
+            "s_cmp_gt_u32 %[lane0], %[l0max]\n\t"                                                   \
+            "s_cbranch_scc1 L%=_x2\n\t"                                                             \
+            "s_branch L%=_top\n"                                                                    \
+            "L%=_nohit:\n\t"                                                                        \
+            "s_bcnt1_i32_b64 %[s0], %[valid]\n\t" /* nk misses: lanes lane0 - 1 .. lane0 + nk - 1 */ \
+            "s_mov_b32 %[dka], 0\n\t"                                                               \
+            "s_mov_b32 %[dkb], 0\n\t"                                                               \
+            "s_add_i32 %[s1], %[lane0], -1\n\t"                                                     \
+            "v_subrev_u32_e32 %[t4], %[s1], %[lane]\n\t"                                            \
+            "v_cmp_ge_u32_e32 vcc, %[s0], %[t4]\n\t"                                                \
+            "s_add_u32 %[s2], %[skip], %[s0]\n\t"                                                   \
+            "s_add_i32 %[s3], %[s2], -1\n\t"                                                        \
+            "v_cndmask_b32_e32 %[t4], %[dummy], %[adr], vcc\n\t"                                    \
+            "ds_write_b16 %[t4], %[word]\n\t"                                                       \
+            "v_lshrrev_b32_e32 %[t4], 1, %[t4]\n\t"                                                 \
+            "ds_write_b8_d16_hi %[t4], %[word] offset:%[tagb]\n\t"                                  \
+            "ds_read_u16 %[ent], %[adr]\n\t"                                                        \
+            "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"                                        \
+            "s_lshr_b32 %[s3], %[s3], 5\n\t" /* the last probe steps by 2 at skip 64 */             \
+            "s_add_u32 %[p], %[q0], %[lane0]\n\t"                                                   \
+            "s_add_u32 %[p], %[p], %[s0]\n\t"                                                       \
+            "s_add_u32 %[p], %[p], %[s3]\n\t"                                                       \
+            "s_add_i32 %[p], %[p], -1\n\t"                                                          \
+            "s_mov_b32 %[skip], %[s2]\n\t"                                                          \
+            "s_cmp_gt_u32 %[skip], %[lsmax]\n\t"                                                    \
+            "s_cbranch_scc1 L%=_x1\n\t"                                                             \
+            "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                        \
+            "s_cbranch_scc1 L%=_x1\n\t"                                                             \
+            "s_sub_u32 %[lane0], %[p], %[q0]\n\t"                                                   \
+            "s_cmp_gt_u32 %[lane0], %[l0max]\n\t"                                                   \
+            "s_cbranch_scc1 L%=_x2\n\t"                                                             \
+            "s_branch L%=_top\n"                                                                    \
+            "L%=_x1:\n\ts_mov_b32 %[code], 1\n\ts_branch L%=_end\n"                                 \
+            "L%=_x2:\n\ts_mov_b32 %[code], 2\n\ts_branch L%=_end\n"                                 \
+            "L%=_x3:\n\ts_mov_b32 %[code], 3\n\ts_branch L%=_end\n"                                 \
+            "L%=_x4:\n\ts_mov_b32 %[code], 4\n\ts_branch L%=_end\n"                                 \
+            "L%=_x5:\n\ts_mov_b32 %[code], 5\n"                                                     \
+            "L%=_end:\n\t"                                                                          \
+            "s_mov_b32 m0, %[m0s]\n\t"                                                              \
+            "s_waitcnt lgkmcnt(0)"                                                                  \
+            : [p] "+s"(p), [skip] "+s"(skip), [lane0] "+s"(lane0), [pend] "+s"(pend), [dka] "+s"(dka), \
+              [dkb] "+s"(dkb), [dkn] "+s"(dkn), [code] "=&s"(code), [f] "=&s"(fx), [c] "=&s"(cx),      \
+              [m0s] "=&s"(_m0s), [pf] "=&s"(_pf), [s0] "=&s"(_s0), [s1] "=&s"(_s1), [s2] "=&s"(_s2),   \
+              [s3] "=&s"(_s3), [valid] "=&s"(_valid), [hm] "=&s"(_hm), [ent] "+v"(e32),              \
+              [entt] "+v"(et32), [tka] "+v"(tka), [tkb] "+v"(tkb), [t0] "=&v"(_t0), [t1] "=&v"(_t1),  \
+              [t2] "=&v"(_t2), [t3] "=&v"(_t3), [t4] "=&v"(_t4)                                       \
+            : [q0] "s"(q0), [L] "s"(L), [lm16] "s"(L - 16), [mwin] "s"(m_win), [dv] "v"(dv),         \
+              [pdl1] "v"(pdl1), [pdc] "v"(pdc), [pdnz] "v"(pdnz), [adr] "v"(adr), [adrt] "v"(adr >> 1), \
+              [word] "v"(word), [lane] "v"(lane), [lane4] "v"(lane << 2), [dummy] "v"(kDummy),         \
+              [skipmax] "i"(64 - DMAX), [dmask] "i"((1u << DMAX) - 1), [lsmax] "i"(64 - SNAPPY_K1R_LSMIN), \
+              [l0max] "i"(62 - SNAPPY_K1R_RMIN), [tagb] "i"(kTagBase), "{v[2:33]}"(g0), "{v[34:65]}"(g1), \
+              "{v[66:97]}"(g2), "{v[98:129]}"(g3)                                                      \
+            : "vcc", "scc", "memory");                                                              \
+    } while (0)
+#elif SNAPPY_K1R_ASM_V == 2
+#define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32)                                                  \
+    do {                                                                                            \
+        uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4;                           \
+        uint64_t _valid, _hm;                                                                       \
+        asm volatile(                                                                               \
+            "s_mov_b32 %[m0s], m0\n\t"                                                              \
+            "s_cmp_gt_u32 %[skip], %[skipmax]\n\t" /* a step of 2 within DMAX probes: C++ round */   \
+            "s_cbranch_scc1 L%=_x3\n"                                                               \
+            "L%=_top:\n\t"                                                                          \
+            "s_lshl_b64 %[valid], %[dmask], %[lane0]\n\t"                                           \
+            "v_cmp_gt_i32_e32 vcc, %[lane0], %[pdl1]\n\t" /* vcc = not in-round */                  \
+            "s_and_b64 %[valid], %[valid], %[mwin]\n\t"                                             \
+            "s_waitcnt lgkmcnt(0)\n\t"                                                              \
+            "v_xor_b32_sdwa %[t0], %[entt], %[word] dst_sel:DWORD dst_unused:UNUSED_PAD "            \
+            "src0_sel:DWORD src1_sel:WORD_1\n\t"                                                    \
+            "v_cndmask_b32_sdwa %[t1], %[pdc], %[ent], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "     \
+            "src0_sel:DWORD src1_sel:WORD_0\n\t" /* the candidate of every lane */                  \
+            "v_cndmask_b32_sdwa %[t0], %[pdnz], %[t0], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "     \
+            "src0_sel:DWORD src1_sel:BYTE_0\n\t"                                                    \
+            "v_cmp_eq_u32_e64 %[hm], 0, %[t0]\n\t"                                                  \
+            "s_and_b64 %[hm], %[hm], %[valid]\n\t"                                                  \
+            "s_cmp_eq_u64 %[hm], 0\n\t"                                                             \
+            "s_cbranch_scc1 L%=_nohit\n\t"                                                          \
+            "s_ff1_i32_b64 %[f], %[hm]\n\t"                                                         \
+            "v_readlane_b32 %[c], %[t1], %[f]\n\t"                                                  \
+            "s_add_u32 %[pf], %[q0], %[f]\n\t"                                                      \
+            "s_and_b32 %[s0], %[pf], -4\n\t"                                                        \
+            "v_add_u32_e32 %[t2], %[s0], %[lane4]\n\t"                                              \
+            "ds_bpermute_b32 %[t2], %[t2], %[dv]\n\t" /* pa: dwords at pf */                        \
+            "s_and_b32 %[c], %[c], 0xffff\n\t"                                                      \
+            "s_lshr_b32 %[s0], %[c], 8\n\t"                                                         \
+            "s_set_gpr_idx_on %[s0], gpr_idx(SRC0)\n\t"                                             \
+            "v_mov_b32_e32 %[t3], v2\n\t"                                                           \
+            "v_mov_b32_e32 %[t4], v3\n\t"                                                           \
+            "s_set_gpr_idx_off\n\t"                                                                 \
+            "s_bfe_u32 %[s1], %[c], 0x60002\n\t"                                                    \
+            "s_lshl_b64 %[hm], -1, %[s1]\n\t" /* lanes >= l0 take register R */                     \
+            "s_and_b32 %[s0], %[c], -4\n\t"                                                         \
+            "v_add_u32_e32 %[t1], %[s0], %[lane4]\n\t"                                              \
+            "v_cndmask_b32_e64 %[t3], %[t4], %[t3], %[hm]\n\t"                                      \
+            "ds_bpermute_b32 %[t3], %[t1], %[t3]\n\t" /* ca: dwords at c */                         \
+            "s_mov_b32 m0, %[pend]\n\t" /* the previous round's token, during the gathers */        \
+            "v_writelane_b32 %[tka], %[dka], m0\n\t"                                                \
+            "v_writelane_b32 %[tkb], %[dkb], m0\n\t"                                                \
+            "s_add_u32 %[pend], %[pend], %[dkn]\n\t"                                                \
+            "s_mov_b32 %[dkn], 0\n\t"                                                               \
+            "s_add_i32 %[s0], %[lane0], -1\n\t"                                                     \
+            "s_cmp_lt_u32 %[lane0], %[f]\n\t"                                                       \
+            "s_cselect_b32 %[s0], %[s0], %[lane0]\n\t" /* lo0 */                                    \
+            "v_subrev_u32_e32 %[t4], %[s0], %[lane]\n\t"                                            \
+            "s_sub_u32 %[s0], %[f], %[s0]\n\t"                                                      \
+            "v_cmp_ge_u32_e32 vcc, %[s0], %[t4]\n\t" /* lanes lo0 .. f insert */                    \
+            "s_and_b32 %[s2], %[pf], 3\n\t"                                                         \
+            "s_mul_i32 %[s2], %[s2], 0xfefefeff\n\t"                                                \
+            "v_cndmask_b32_e32 %[t4], %[dummy], %[adr], vcc\n\t"                                    \
+            "ds_write_b16 %[t4], %[word]\n\t"                                                       \
+            "v_lshrrev_b32_e32 %[t4], 1, %[t4]\n\t"                                                 \
+            "ds_write_b8_d16_hi %[t4], %[word] offset:%[tagb]\n\t"                                  \
+            "ds_read_u16 %[ent], %[adr]\n\t"                                                        \
+            "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"                                        \
+            "s_add_i32 %[s2], %[s2], 0x7060504\n\t"                                                 \
+            "s_and_b32 %[s3], %[c], 3\n\t"                                                          \
+            "s_mul_i32 %[s3], %[s3], 0xfefefeff\n\t"                                                \
+            "s_add_i32 %[s3], %[s3], 0x7060504\n\t"                                                 \
+            "s_waitcnt lgkmcnt(2)\n\t" /* pa, ca and the inserts; the entry reads stay in flight */ \
+            "v_mov_b32_dpp %[t1], %[t2] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
+            "v_mov_b32_dpp %[t4], %[t3] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
+            "v_perm_b32 %[t2], %[t2], %[t1], %[s2]\n\t"                                             \
+            "v_perm_b32 %[t3], %[t3], %[t4], %[s3]\n\t"                                             \
+            "v_cmp_ne_u32_e32 vcc, %[t2], %[t3]\n\t"                                                \
+            "v_xor_b32_e32 %[t2], %[t2], %[t3]\n\t"                                                 \
+            "v_or_b32_e32 %[t2], 1, %[t2]\n\t"                                                      \
+            "v_ffbh_u32_e32 %[t2], %[t2]\n\t"                                                       \
+            "v_lshrrev_b32_e32 %[t2], 3, %[t2]\n\t"                                                 \
+            "v_or_b32_e32 %[t2], %[t2], %[lane4]\n\t" /* the prefix length if this dword differs */ \
+            "s_and_b32 %[s1], vcc_lo, 0xffff\n\t"                                                   \
+            "s_cmp_eq_u32 %[s1], 0\n\t"                                                             \
+            "s_cbranch_scc1 L%=_x4\n\t"                                                             \
+            "s_ff1_i32_b32 %[s1], %[s1]\n\t"                                                        \
+            "s_nop 1\n\t"                                                                           \
+            "v_readlane_b32 %[s0], %[t2], %[s1]\n\t"                                                \
+            "s_sub_u32 %[s1], %[L], %[pf]\n\t"                                                      \
+            "s_min_u32 %[s0], %[s0], %[s1]\n\t"                                                     \
+            "s_cmp_lt_u32 %[s0], 4\n\t"                                                             \
+            "s_cbranch_scc1 L%=_x5\n\t"                                                             \
+            "s_add_u32 %[p], %[pf], %[s0]\n\t"                                                      \
+            "s_sub_u32 %[lane0], %[p], %[q0]\n\t"                                                   \
+            "s_lshl_b32 %[s1], %[s0], 16\n\t"                                                       \
+            "s_or_b32 %[dka], %[s1], %[pf]\n\t"                                                     \
+            "s_sub_u32 %[dkb], %[pf], %[c]\n\t"                                                     \
+            "s_mov_b32 %[dkn], 1\n\t"                                                               \
+            "s_mov_b32 %[skip], 32\n\t"                                                             \
+            "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                        \
+            "s_cbranch_scc1 L%=_x1\n\t"                                                             \
+            "s_cmp_le_u32 %[lane0], %[l0max]\n\t"                                                   \
+            "s_cbranch_scc1 L%=_top\n\t"                                                            \
+            "s_branch L%=_x2\n"                                                                     \
+            "L%=_nohit:\n\t"                                                                        \
+            "s_bcnt1_i32_b64 %[s0], %[valid]\n\t" /* nk misses: lanes lane0 - 1 .. lane0 + nk - 1 */ \
+            "s_mov_b32 m0, %[pend]\n\t"                                                             \
+            "v_writelane_b32 %[tka], %[dka], m0\n\t"                                                \
+            "v_writelane_b32 %[tkb], %[dkb], m0\n\t"                                                \
+            "s_add_u32 %[pend], %[pend], %[dkn]\n\t"                                                \
+            "s_mov_b32 %[dkn], 0\n\t"                                                               \
+            "s_mov_b32 %[dka], 0\n\t"                                                               \
+            "s_mov_b32 %[dkb], 0\n\t"                                                               \
+            "s_add_i32 %[s1], %[lane0], -1\n\t"                                                     \
+            "v_subrev_u32_e32 %[t4], %[s1], %[lane]\n\t"                                            \
+            "v_cmp_ge_u32_e32 vcc, %[s0], %[t4]\n\t"                                                \
+            "s_add_u32 %[s2], %[skip], %[s0]\n\t"                                                   \
+            "s_add_i32 %[s3], %[s2], -1\n\t"                                                        \
+            "v_cndmask_b32_e32 %[t4], %[dummy], %[adr], vcc\n\t"                                    \
+            "ds_write_b16 %[t4], %[word]\n\t"                                                       \
+            "v_lshrrev_b32_e32 %[t4], 1, %[t4]\n\t"                                                 \
+            "ds_write_b8_d16_hi %[t4], %[word] offset:%[tagb]\n\t"                                  \
+            "ds_read_u16 %[ent], %[adr]\n\t"                                                        \
+            "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"                                        \
+            "s_lshr_b32 %[s3], %[s3], 5\n\t" /* the last probe steps by 2 at skip 64 */             \
+            "s_add_u32 %[p], %[q0], %[lane0]\n\t"                                                   \
+            "s_add_u32 %[p], %[p], %[s0]\n\t"                                                       \
+            "s_add_u32 %[p], %[p], %[s3]\n\t"                                                       \
+            "s_add_i32 %[p], %[p], -1\n\t"                                                          \
+            "s_mov_b32 %[skip], %[s2]\n\t"                                                          \
+            "s_cmp_gt_u32 %[skip], %[lsmax]\n\t"                                                    \
+            "s_cbranch_scc1 L%=_x1\n\t"                                                             \
+            "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                        \
+            "s_cbranch_scc1 L%=_x1\n\t"                                                             \
+            "s_sub_u32 %[lane0], %[p], %[q0]\n\t"                                                   \
+            "s_cmp_gt_u32 %[lane0], %[l0max]\n\t"                                                   \
+            "s_cbranch_scc1 L%=_x2\n\t"                                                             \
+            "s_cmp_le_u32 %[skip], %[skipmax]\n\t"                                                  \
+            "s_cbranch_scc1 L%=_top\n"                                                              \
+            "L%=_x3:\n\ts_mov_b32 %[code], 3\n\ts_branch L%=_end\n"                                 \
+            "L%=_x1:\n\ts_mov_b32 %[code], 1\n\ts_branch L%=_end\n"                                 \
+            "L%=_x2:\n\ts_mov_b32 %[code], 2\n\ts_branch L%=_end\n"                                 \
+            "L%=_x4:\n\ts_mov_b32 %[code], 4\n\ts_branch L%=_end\n"                                 \
+            "L%=_x5:\n\ts_mov_b32 %[code], 5\n"                                                     \
+            "L%=_end:\n\t"                                                                          \
+            "s_mov_b32 m0, %[m0s]\n\t"                                                              \
+            "s_waitcnt lgkmcnt(0)"                                                                  \
+            : [p] "+s"(p), [skip] "+s"(skip), [lane0] "+s"(lane0), [pend] "+s"(pend), [dka] "+s"(dka), \
+              [dkb] "+s"(dkb), [dkn] "+s"(dkn), [code] "=&s"(code), [f] "=&s"(fx), [c] "=&s"(cx),      \
+              [m0s] "=&s"(_m0s), [pf] "=&s"(_pf), [s0] "=&s"(_s0), [s1] "=&s"(_s1), [s2] "=&s"(_s2),   \
+              [s3] "=&s"(_s3), [valid] "=&s"(_valid), [hm] "=&s"(_hm), [ent] "+v"(e32),              \
+              [entt] "+v"(et32), [tka] "+v"(tka), [tkb] "+v"(tkb), [t0] "=&v"(_t0), [t1] "=&v"(_t1),  \
+              [t2] "=&v"(_t2), [t3] "=&v"(_t3), [t4] "=&v"(_t4)                                       \
+            : [q0] "s"(q0), [L] "s"(L), [lm16] "s"(L - 16), [mwin] "s"(m_win), [dv] "v"(dv),         \
+              [pdl1] "v"(pdl1), [pdc] "v"(pdc), [pdnz] "v"(pdnz), [adr] "v"(adr), [adrt] "v"(adr >> 1), \
+              [word] "v"(word), [lane] "v"(lane), [lane4] "v"(lane << 2), [dummy] "v"(kDummy),         \
+              [skipmax] "i"(64 - DMAX), [dmask] "i"((1u << DMAX) - 1), [lsmax] "i"(64 - SNAPPY_K1R_LSMIN), \
+              [l0max] "i"(62 - SNAPPY_K1R_RMIN), [tagb] "i"(kTagBase), "{v[2:33]}"(g0), "{v[34:65]}"(g1), \
+              "{v[66:97]}"(g2), "{v[98:129]}"(g3)                                                      \
+            : "vcc", "scc", "memory");                                                              \
+    } while (0)
+#elif SNAPPY_K1R_ASM_V == 3
+#define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32)                                                  \
+    do {                                                                                            \
+        uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4, _t5, _t6;                           \
+        uint64_t _valid, _hm;                                                                       \
+        asm volatile(                                                                               \
+            "s_mov_b32 %[m0s], m0\n\t"                                                              \
+            "s_cmp_gt_u32 %[skip], %[skipmax]\n\t" /* a step of 2 within DMAX probes: C++ round */   \
+            "s_cbranch_scc1 L%=_x3\n"                                                               \
+            "L%=_top:\n\t"                                                                          \
+            "s_lshl_b64 %[valid], %[dmask], %[lane0]\n\t"                                           \
+            "s_add_u32 %[pf], %[q0], %[lane0]\n\t" /* the first probe: 60 % of matches (text) */     \
+            "s_and_b32 %[s0], %[pf], -4\n\t"                                                        \
+            "v_add_u32_e32 %[t2], %[s0], %[lane4]\n\t"                                              \
+            "ds_bpermute_b32 %[t5], %[t2], %[dv]\n\t" /* pa at the first probe */                   \
+            "v_cmp_gt_i32_e32 vcc, %[lane0], %[pdl1]\n\t" /* vcc = not in-round */                  \
+            "s_and_b64 %[valid], %[valid], %[mwin]\n\t"                                             \
+            "s_waitcnt lgkmcnt(1)\n\t" /* the entries (pa stays in flight) */                        \
+            "v_readlane_b32 %[c], %[ent], %[lane0]\n\t" /* its candidate: its entry */              \
+            "v_xor_b32_sdwa %[t0], %[entt], %[word] dst_sel:DWORD dst_unused:UNUSED_PAD "            \
+            "src0_sel:DWORD src1_sel:WORD_1\n\t"                                                    \
+            "v_cndmask_b32_sdwa %[t1], %[pdc], %[ent], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "     \
+            "src0_sel:DWORD src1_sel:WORD_0\n\t" /* the candidate of every lane */                  \
+            "v_cndmask_b32_sdwa %[t0], %[pdnz], %[t0], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "     \
+            "src0_sel:DWORD src1_sel:BYTE_0\n\t"                                                    \
+            "s_lshr_b32 %[s0], %[c], 8\n\t"                                                         \
+            "s_set_gpr_idx_on %[s0], gpr_idx(SRC0)\n\t"                                             \
+            "v_mov_b32_e32 %[t3], v2\n\t"                                                           \
+            "v_mov_b32_e32 %[t4], v3\n\t"                                                           \
+            "s_set_gpr_idx_off\n\t"                                                                 \
+            "s_bfe_u32 %[s1], %[c], 0x60002\n\t"                                                    \
+            "s_lshl_b64 %[hm], -1, %[s1]\n\t" /* lanes >= l0 take register R */                     \
+            "s_and_b32 %[s0], %[c], -4\n\t"                                                         \
+            "v_add_u32_e32 %[t2], %[s0], %[lane4]\n\t"                                              \
+            "v_cndmask_b32_e64 %[t3], %[t4], %[t3], %[hm]\n\t"                                      \
+            "ds_bpermute_b32 %[t6], %[t2], %[t3]\n\t" /* ca at the first probe's candidate */       \
+            "v_cmp_eq_u32_e64 %[hm], 0, %[t0]\n\t"                                                  \
+            "s_and_b64 %[hm], %[hm], %[valid]\n\t"                                                  \
+            "s_cmp_eq_u64 %[hm], 0\n\t"                                                             \
+            "s_cbranch_scc1 L%=_nohit\n\t"                                                          \
+            "s_ff1_i32_b64 %[f], %[hm]\n\t"                                                         \
+            "s_cmp_eq_u32 %[f], %[lane0]\n\t"                                                       \
+            "s_cbranch_scc1 L%=_hit\n\t"                                                            \
+            /* a later probe hits: its gathers, once the first probe's have landed */               \
+            "s_add_u32 %[pf], %[q0], %[f]\n\t"                                                      \
+            "v_readlane_b32 %[c], %[t1], %[f]\n\t"                                                  \
+            "s_and_b32 %[s0], %[pf], -4\n\t"                                                        \
+            "v_add_u32_e32 %[t2], %[s0], %[lane4]\n\t"                                              \
+            "s_waitcnt lgkmcnt(0)\n\t"                                                              \
+            "ds_bpermute_b32 %[t5], %[t2], %[dv]\n\t" /* pa: dwords at pf */                        \
+            "s_lshr_b32 %[s0], %[c], 8\n\t"                                                         \
+            "s_set_gpr_idx_on %[s0], gpr_idx(SRC0)\n\t"                                             \
+            "v_mov_b32_e32 %[t3], v2\n\t"                                                           \
+            "v_mov_b32_e32 %[t4], v3\n\t"                                                           \
+            "s_set_gpr_idx_off\n\t"                                                                 \
+            "s_bfe_u32 %[s1], %[c], 0x60002\n\t"                                                    \
+            "s_lshl_b64 %[hm], -1, %[s1]\n\t"                                                       \
+            "s_and_b32 %[s0], %[c], -4\n\t"                                                         \
+            "v_add_u32_e32 %[t2], %[s0], %[lane4]\n\t"                                              \
+            "v_cndmask_b32_e64 %[t3], %[t4], %[t3], %[hm]\n\t"                                      \
+            "ds_bpermute_b32 %[t6], %[t2], %[t3]\n"  /* ca: dwords at c */                          \
+            "L%=_hit:\n\t"                                                                          \
+            "s_mov_b32 m0, %[pend]\n\t" /* the previous round's token, during the gathers */        \
+            "v_writelane_b32 %[tka], %[dka], m0\n\t"                                                \
+            "v_writelane_b32 %[tkb], %[dkb], m0\n\t"                                                \
+            "s_add_u32 %[pend], %[pend], %[dkn]\n\t"                                                \
+            "s_mov_b32 %[dkn], 0\n\t"                                                               \
+            "s_add_i32 %[s0], %[lane0], -1\n\t"                                                     \
+            "s_cmp_lt_u32 %[lane0], %[f]\n\t"                                                       \
+            "s_cselect_b32 %[s0], %[s0], %[lane0]\n\t" /* lo0 */                                    \
+            "v_subrev_u32_e32 %[t4], %[s0], %[lane]\n\t"                                            \
+            "s_sub_u32 %[s0], %[f], %[s0]\n\t"                                                      \
+            "v_cmp_ge_u32_e32 vcc, %[s0], %[t4]\n\t" /* lanes lo0 .. f insert */                    \
+            "s_and_b32 %[s2], %[pf], 3\n\t"                                                         \
+            "s_mul_i32 %[s2], %[s2], 0xfefefeff\n\t"                                                \
+            "v_cndmask_b32_e32 %[t4], %[dummy], %[adr], vcc\n\t"                                    \
+            "ds_write_b16 %[t4], %[word]\n\t"                                                       \
+            "v_lshrrev_b32_e32 %[t4], 1, %[t4]\n\t"                                                 \
+            "ds_write_b8_d16_hi %[t4], %[word] offset:%[tagb]\n\t"                                  \
+            "ds_read_u16 %[ent], %[adr]\n\t"                                                        \
+            "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"                                        \
+            "s_add_i32 %[s2], %[s2], 0x7060504\n\t"                                                 \
+            "s_and_b32 %[s3], %[c], 3\n\t"                                                          \
+            "s_mul_i32 %[s3], %[s3], 0xfefefeff\n\t"                                                \
+            "s_add_i32 %[s3], %[s3], 0x7060504\n\t"                                                 \
+            "s_waitcnt lgkmcnt(2)\n\t" /* pa, ca and the inserts; the entry reads stay in flight */ \
+            "v_mov_b32_dpp %[t1], %[t5] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
+            "v_mov_b32_dpp %[t4], %[t6] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
+            "v_perm_b32 %[t2], %[t5], %[t1], %[s2]\n\t"                                             \
+            "v_perm_b32 %[t3], %[t6], %[t4], %[s3]\n\t"                                             \
+            "v_cmp_ne_u32_e32 vcc, %[t2], %[t3]\n\t"                                                \
+            "v_xor_b32_e32 %[t2], %[t2], %[t3]\n\t"                                                 \
+            "v_or_b32_e32 %[t2], 1, %[t2]\n\t"                                                      \
+            "v_ffbh_u32_e32 %[t2], %[t2]\n\t"                                                       \
+            "v_lshrrev_b32_e32 %[t2], 3, %[t2]\n\t"                                                 \
+            "v_or_b32_e32 %[t2], %[t2], %[lane4]\n\t" /* the prefix length if this dword differs */ \
+            "s_and_b32 %[s1], vcc_lo, 0xffff\n\t"                                                   \
+            "s_cmp_eq_u32 %[s1], 0\n\t"                                                             \
+            "s_cbranch_scc1 L%=_x4\n\t"                                                             \
+            "s_ff1_i32_b32 %[s1], %[s1]\n\t"                                                        \
+            "s_nop 1\n\t"                                                                           \
+            "v_readlane_b32 %[s0], %[t2], %[s1]\n\t"                                                \
+            "s_sub_u32 %[s1], %[L], %[pf]\n\t"                                                      \
+            "s_min_u32 %[s0], %[s0], %[s1]\n\t"                                                     \
+            "s_cmp_lt_u32 %[s0], 4\n\t"                                                             \
+            "s_cbranch_scc1 L%=_x5\n\t"                                                             \
+            "s_add_u32 %[p], %[pf], %[s0]\n\t"                                                      \
+            "s_sub_u32 %[lane0], %[p], %[q0]\n\t"                                                   \
+            "s_lshl_b32 %[s1], %[s0], 16\n\t"                                                       \
+            "s_or_b32 %[dka], %[s1], %[pf]\n\t"                                                     \
+            "s_sub_u32 %[dkb], %[pf], %[c]\n\t"                                                     \
+            "s_mov_b32 %[dkn], 1\n\t"                                                               \
+            "s_mov_b32 %[skip], 32\n\t"                                                             \
+            "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                        \
+            "s_cbranch_scc1 L%=_x1\n\t"                                                             \
+            "s_cmp_le_u32 %[lane0], %[l0max]\n\t"                                                   \
+            "s_cbranch_scc1 L%=_top\n\t"                                                            \
+            "s_branch L%=_x2\n"                                                                     \
+            "L%=_nohit:\n\t"                                                                        \
+            "s_bcnt1_i32_b64 %[s0], %[valid]\n\t" /* nk misses: lanes lane0 - 1 .. lane0 + nk - 1 */ \
+            "s_mov_b32 m0, %[pend]\n\t"                                                             \
+            "v_writelane_b32 %[tka], %[dka], m0\n\t"                                                \
+            "v_writelane_b32 %[tkb], %[dkb], m0\n\t"                                                \
+            "s_add_u32 %[pend], %[pend], %[dkn]\n\t"                                                \
+            "s_mov_b32 %[dkn], 0\n\t"                                                               \
+            "s_mov_b32 %[dka], 0\n\t"                                                               \
+            "s_mov_b32 %[dkb], 0\n\t"                                                               \
+            "s_add_i32 %[s1], %[lane0], -1\n\t"                                                     \
+            "v_subrev_u32_e32 %[t4], %[s1], %[lane]\n\t"                                            \
+            "v_cmp_ge_u32_e32 vcc, %[s0], %[t4]\n\t"                                                \
+            "s_add_u32 %[s2], %[skip], %[s0]\n\t"                                                   \
+            "s_add_i32 %[s3], %[s2], -1\n\t"                                                        \
+            "v_cndmask_b32_e32 %[t4], %[dummy], %[adr], vcc\n\t"                                    \
+            "ds_write_b16 %[t4], %[word]\n\t"                                                       \
+            "v_lshrrev_b32_e32 %[t4], 1, %[t4]\n\t"                                                 \
+            "ds_write_b8_d16_hi %[t4], %[word] offset:%[tagb]\n\t"                                  \
+            "ds_read_u16 %[ent], %[adr]\n\t"                                                        \
+            "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"                                        \
+            "s_lshr_b32 %[s3], %[s3], 5\n\t" /* the last probe steps by 2 at skip 64 */             \
+            "s_add_u32 %[p], %[q0], %[lane0]\n\t"                                                   \
+            "s_add_u32 %[p], %[p], %[s0]\n\t"                                                       \
+            "s_add_u32 %[p], %[p], %[s3]\n\t"                                                       \
+            "s_add_i32 %[p], %[p], -1\n\t"                                                          \
+            "s_mov_b32 %[skip], %[s2]\n\t"                                                          \
+            "s_cmp_gt_u32 %[skip], %[lsmax]\n\t"                                                    \
+            "s_cbranch_scc1 L%=_x1\n\t"                                                             \
+            "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                        \
+            "s_cbranch_scc1 L%=_x1\n\t"                                                             \
+            "s_sub_u32 %[lane0], %[p], %[q0]\n\t"                                                   \
+            "s_cmp_gt_u32 %[lane0], %[l0max]\n\t"                                                   \
+            "s_cbranch_scc1 L%=_x2\n\t"                                                             \
+            "s_cmp_le_u32 %[skip], %[skipmax]\n\t"                                                  \
+            "s_cbranch_scc1 L%=_top\n"                                                              \
+            "L%=_x3:\n\ts_mov_b32 %[code], 3\n\ts_branch L%=_end\n"                                 \
+            "L%=_x1:\n\ts_mov_b32 %[code], 1\n\ts_branch L%=_end\n"                                 \
+            "L%=_x2:\n\ts_mov_b32 %[code], 2\n\ts_branch L%=_end\n"                                 \
+            "L%=_x4:\n\ts_mov_b32 %[code], 4\n\ts_branch L%=_end\n"                                 \
+            "L%=_x5:\n\ts_mov_b32 %[code], 5\n"                                                     \
+            "L%=_end:\n\t"                                                                          \
+            "s_mov_b32 m0, %[m0s]\n\t"                                                              \
+            "s_waitcnt lgkmcnt(0)"                                                                  \
+            : [p] "+s"(p), [skip] "+s"(skip), [lane0] "+s"(lane0), [pend] "+s"(pend), [dka] "+s"(dka), \
+              [dkb] "+s"(dkb), [dkn] "+s"(dkn), [code] "=&s"(code), [f] "=&s"(fx), [c] "=&s"(cx),      \
+              [m0s] "=&s"(_m0s), [pf] "=&s"(_pf), [s0] "=&s"(_s0), [s1] "=&s"(_s1), [s2] "=&s"(_s2),   \
+              [s3] "=&s"(_s3), [valid] "=&s"(_valid), [hm] "=&s"(_hm), [ent] "+v"(e32),              \
+              [entt] "+v"(et32), [tka] "+v"(tka), [tkb] "+v"(tkb), [t0] "=&v"(_t0), [t1] "=&v"(_t1),  \
+              [t2] "=&v"(_t2), [t3] "=&v"(_t3), [t4] "=&v"(_t4), [t5] "=&v"(_t5), [t6] "=&v"(_t6)                                       \
+            : [q0] "s"(q0), [L] "s"(L), [lm16] "s"(L - 16), [mwin] "s"(m_win), [dv] "v"(dv),         \
+              [pdl1] "v"(pdl1), [pdc] "v"(pdc), [pdnz] "v"(pdnz), [adr] "v"(adr), [adrt] "v"(adr >> 1), \
+              [word] "v"(word), [lane] "v"(lane), [lane4] "v"(lane << 2), [dummy] "v"(kDummy),         \
+              [skipmax] "i"(64 - DMAX), [dmask] "i"((1u << DMAX) - 1), [lsmax] "i"(64 - SNAPPY_K1R_LSMIN), \
+              [l0max] "i"(62 - SNAPPY_K1R_RMIN), [tagb] "i"(kTagBase), "{v[2:33]}"(g0), "{v[34:65]}"(g1), \
+              "{v[66:97]}"(g2), "{v[98:129]}"(g3)                                                      \
+            : "vcc", "scc", "memory");                                                              \
+    } while (0)
+#endif
 #if defined(SNAPPY_K1R_LSTAMPS)
     uint64_t seg[6] = {0, 0, 0, 0, 0, 0};
     uint64_t s0, s1, s2, s3, s4, s5, s6;
@@ -748,6 +1260,54 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             // SNAPPY_K1R_LATE_ENT reads at the round's end instead)
             TBL_READ_ENT(adr);
             for (;;) {
+#if K1R_ASM_ROUNDS
+                if constexpr (!BIG) {
+                    // the common rounds as one hand-scheduled loop (k1r_asm_rounds below)
+                    uint32_t code, fx, cx;
+                    uint32_t e32 = ent, et32 = ent_t;
+                    K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32);
+                    ent = (uint16_t)e32;
+                    ent_t = (uint8_t)et32;
+                    if (code == 1) break;  // skip past the step-1 range, or is_block_end
+                    if (code == 2) {       // the window needs to move
+                        refresh();
+                        lane0 = 1;
+                        TBL_READ_ENT(adr);
+                        continue;
+                    }
+                    if (code >= 4) {  // the round stopped after its inserts: finish it here
+                        const uint32_t f = fx, pf = q0 + fx, c = cx;
+                        uint32_t np;
+                        if (code == 4) {  // 64 or more equal bytes: extend the match
+                            uint32_t len = __builtin_elementwise_min(match_len_from(pf, c, 64), L - pf);
+                            dka = pf | (len << 16);
+                            dkb = pf - c;
+                            dkn = 1;
+                            np = pf + len;
+                            skip = 32;
+                        } else {  // tag collision: a miss (as in the C++ round below)
+                            dkn = 0;
+                            if (f == lane0) {
+                                TBL_INSERT(lane - (lane0 - 1) <= 1);
+                                LDS_ORDER();
+                                TBL_READ_ENT(adr);
+                            }
+                            np = pf + ((skip + f - lane0) >> 5);
+                            skip += f - lane0 + 1;
+                        }
+                        p = np;
+                        if (!(skip <= 64 - SNAPPY_K1R_LSMIN && p <= L - 16)) break;
+                        lane0 = p - q0;
+                        if (lane0 + SNAPPY_K1R_RMIN > 62) {
+                            refresh();
+                            lane0 = 1;
+                            TBL_READ_ENT(adr);
+                        }
+                        continue;
+                    }
+                    // code 3: a round whose probes reach a step of 2 (skip > 64 - DMAX) runs below
+                }
+#endif
                 LSTAMP(s0);
                 drain_token();  // the previous round's match: one writelane pair per round
                 // probe k = lane - lane0 for k <= kcap: step 1 before it ((skip + k - 1) >> 5 == 1),
@@ -1758,70 +2318,108 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             __builtin_amdgcn_wave_barrier();
             pre = load_seg(comp, B + 512, c1, lane);
         }
-        // ---- lane-parallel candidate parse: an element starting at o + lane
-        const uint32_t q = o + lane;  // < 320
-        const uint32_t qa = WADR(q);
-        // two aligned dwords (one ds_read2_b32; unaligned LDS reads measured slower)
-        const uint32_t dA = w32[qa >> 2], dB = w32[(qa >> 2) + 1];
-        const uint32_t sh = 8 * (qa & 3);
-        const uint32_t x0 = __builtin_amdgcn_alignbit(dB, dA, sh);  // tag, t1, t2, t3 (sh = 0: dA)
-        const uint32_t x1 = dB >> sh;  // t4 in bits 0..7 (the only byte used: b4 below)
-        const uint32_t tag = x0 & 0xFF;
-        uint32_t size, olen, info;  // info: copy offset, or literal header length
-        const uint32_t t = tag & 3;
-        {  // tag dispatch in selects of precomputed values (no exec-mask branches;
-           // src/snappy_decompression.c:290-333)
-            const uint32_t m = tag >> 2;
-            const uint32_t b4 = __builtin_amdgcn_alignbit(x1, x0, 8);  // bytes 1..4
-            const uint32_t k = __builtin_elementwise_sub_sat(m, 59u);  // literal: extra length bytes
-            const uint32_t lx = b4 & (0xFFFFFFFFu >> ((32 - 8 * k) & 31));
-            const uint32_t lv = k ? lx : m;
-            const uint32_t l_olen = lv + 1, c1_olen = (m & 7) + 4, c_olen = m + 1;
-            const uint32_t c1b = ((tag >> 5) << 8) | (b4 & 0xFF), c2b = b4 & 0xFFFF, l_info = 1 + k;
-            const uint32_t l_size = lv + k + 2, c_size = (0x5320u >> (4 * t)) & 0xF;  // copies: 2, 3, 5 bytes
-            const bool is_l = t == 0, is_c1 = t == 1, is_c2 = t == 2;
-            const uint32_t cx_olen = is_c1 ? c1_olen : c_olen;
-            olen = is_l ? l_olen : cx_olen;  // garbage lengths are clamped below
-            const uint32_t c24 = is_c2 ? c2b : b4;
-            const uint32_t cx_info = is_c1 ? c1b : c24;
-            info = is_l ? l_info : cx_info;
-            size = is_l ? l_size : c_size;
-        }
+        // ---- a batch parses up to two 64-position halves of the window: half A
+        // at o, half B at o + xa, where A's element chain leaves its 64
+        // positions.  The two chains' elements are merged into lanes 0 .. E - 1
+        // (E <= 64) and decoded once: the per-element work (decode, scans,
+        // validity, the passes' setup) runs on up to twice the elements, and the
+        // byte passes over up to twice the output.
         K4STAMP(tb);
-        // ---- element chain from lane 0 by pointer doubling: J^k(0) for lane k.
-        // Positions are kept as ds_bpermute addresses (4 x position); one >= 256
-        // has left the window: its bpermute result is discarded, so no masking
-        const uint32_t J1 = 4 * lane + 4 * (size < 64 ? size : 64);
+        uint32_t ex0, eb4, E;  // merged element k at lane k: its bytes 0..3 and 1..4
+        {
+            // lane l <- the bytes at window position ho + l (two aligned dwords: one
+            // ds_read2_b32; unaligned LDS reads measured slower), its element size,
+            // then the element chain from ho by pointer doubling (lane k <- element
+            // k: bytes, count; the position after the last one in the 64, xa)
+            auto parse_half = [&](uint32_t ho, uint32_t &hx0, uint32_t &hb4, uint32_t &hE, uint32_t &hexit) {
+                const uint32_t qa = WADR(ho + lane);
+                const uint32_t dA = w32[qa >> 2], dB = w32[(qa >> 2) + 1];
+                const uint32_t sh = 8 * (qa & 3);
+                const uint32_t x0 = __builtin_amdgcn_alignbit(dB, dA, sh);      // tag, t1, t2, t3
+                const uint32_t b4 = __builtin_amdgcn_alignbit(dB >> sh, x0, 8);  // t1 .. t4
+                // element size: literal 1 + k + (length - 1) + 1, copies 2 / 3 / 5
+                // (src/snappy_decompression.c:290-333)
+                const uint32_t tag = x0 & 0xFF, m = tag >> 2, t = tag & 3;
+                const uint32_t k = __builtin_elementwise_sub_sat(m, 59u);
+                const uint32_t lv = k ? b4 & (0xFFFFFFFFu >> ((32 - 8 * k) & 31)) : m;
+                const uint32_t size = t == 0 ? lv + k + 2 : (0x5320u >> (4 * t)) & 0xF;
+                // positions as ds_bpermute addresses (4 x position); one >= 256 has
+                // left the 64: its bpermute result is discarded, so no masking
+                const uint32_t J1 = 4 * lane + 4 * (size < 64 ? size : 64);
 #define JUMP(T, a) ({ const uint32_t _a = (a);                                            \
         const uint32_t _g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)_a, (int)(T));     \
         _a < 256 ? _g : _a; })
-        const uint32_t J2 = JUMP(J1, J1);
-        const uint32_t J4 = JUMP(J2, J2);
-        const uint32_t J8 = JUMP(J4, J4);
-        const uint32_t J16 = JUMP(J8, J8);
-        // (bpermute must run with every lane active: select afterwards).  An
-        // element is at least 2 bytes, so 64 positions hold at most 32
-        // elements: lanes >= 32 (copies of lanes 0-31) are out of the batch
-        uint32_t pos4 = 0;
-        { const uint32_t g = JUMP(J1, pos4); pos4 = (lane & 1) ? g : pos4; }
-        { const uint32_t g = JUMP(J2, pos4); pos4 = (lane & 2) ? g : pos4; }
-        { const uint32_t g = JUMP(J4, pos4); pos4 = (lane & 4) ? g : pos4; }
-        { const uint32_t g = JUMP(J8, pos4); pos4 = (lane & 8) ? g : pos4; }
-        { const uint32_t g = JUMP(J16, pos4); pos4 = (lane & 16) ? g : pos4; }
+                const uint32_t J2 = JUMP(J1, J1);
+                const uint32_t J4 = JUMP(J2, J2);
+                const uint32_t J8 = JUMP(J4, J4);
+                const uint32_t J16 = JUMP(J8, J8);
+                // (bpermute must run with every lane active: select afterwards).  An
+                // element is at least 2 bytes, so 64 positions hold at most 32
+                // elements: lanes >= 32 (copies of lanes 0-31) are out of the half
+                uint32_t pos4 = 0;
+                { const uint32_t g = JUMP(J1, pos4); pos4 = (lane & 1) ? g : pos4; }
+                { const uint32_t g = JUMP(J2, pos4); pos4 = (lane & 2) ? g : pos4; }
+                { const uint32_t g = JUMP(J4, pos4); pos4 = (lane & 4) ? g : pos4; }
+                { const uint32_t g = JUMP(J8, pos4); pos4 = (lane & 8) ? g : pos4; }
+                { const uint32_t g = JUMP(J16, pos4); pos4 = (lane & 16) ? g : pos4; }
 #undef JUMP
-        // lane k < E holds element k of the batch (starts are increasing);
-        // lanes >= E gather garbage, masked by `live` / nexec below
-        uint32_t E = (uint32_t)__builtin_popcountll(__ballot(pos4 < 256) & 0xFFFFFFFFull);
-        const uint32_t e_t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)pos4, (int)t);
-        const uint32_t e_size = (uint32_t)__builtin_amdgcn_ds_bpermute((int)pos4, (int)size);
-        uint32_t e_len = (uint32_t)__builtin_amdgcn_ds_bpermute((int)pos4, (int)olen);
-        const uint32_t e_info = (uint32_t)__builtin_amdgcn_ds_bpermute((int)pos4, (int)info);
+                hE = (uint32_t)__builtin_popcountll(__ballot(pos4 < 256) & 0xFFFFFFFFull);  // >= 1
+                hx0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)pos4, (int)x0);
+                hb4 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)pos4, (int)b4);
+                const uint32_t last = (uint32_t)__builtin_amdgcn_readlane(pos4, hE - 1) >> 2;
+                hexit = last + (uint32_t)__builtin_amdgcn_readlane(size, last);
+            };
+            uint32_t ax0, ab4, ea, xa;
+            parse_half(o, ax0, ab4, ea, xa);
+            ex0 = ax0;
+            eb4 = ab4;
+            E = ea;
+            // half B when its 64 positions and their 5 bytes stay in the valid
+            // window (bytes [0, 512) from B: o + xa + 63 + 5 < 512)
+#ifndef SNAPPY_K4_HALVES
+#define SNAPPY_K4_HALVES 2  // 1: one 64-position half per batch (round 3's batch size)
+#endif
+            if (SNAPPY_K4_HALVES > 1 && o + xa <= 440) {
+                uint32_t bx0, bb4, eb, xb;
+                parse_half(o + xa, bx0, bb4, eb, xb);
+                (void)xb;
+                // lanes >= ea take B's element lane - ea
+                const int sa = (int)(4 * (lane - ea));
+                const uint32_t sx0 = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)bx0);
+                const uint32_t sb4 = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)bb4);
+                const bool fa = lane < ea;
+                ex0 = fa ? ax0 : sx0;
+                eb4 = fa ? ab4 : sb4;
+                E = ea + eb;
+            }
+        }
+        // lane k < E holds element k of the batch; lanes >= E hold garbage,
+        // masked by `live` / nexec below.  Decode: tag dispatch as selects of
+        // precomputed values (no exec-mask branches; src/snappy_decompression.c:290-333)
+        uint32_t e_t, e_size, e_len, e_info;  // e_info: copy offset, or literal header length
+        {
+            const uint32_t tag = ex0 & 0xFF, m = tag >> 2;
+            e_t = tag & 3;
+            const uint32_t k = __builtin_elementwise_sub_sat(m, 59u);  // literal: extra length bytes
+            const uint32_t lx = eb4 & (0xFFFFFFFFu >> ((32 - 8 * k) & 31));
+            const uint32_t lv = k ? lx : m;
+            const uint32_t l_olen = lv + 1, c1_olen = (m & 7) + 4, c_olen = m + 1;
+            const uint32_t c1b = ((tag >> 5) << 8) | (eb4 & 0xFF), c2b = eb4 & 0xFFFF, l_info = 1 + k;
+            const uint32_t l_size = lv + k + 2, c_size = (0x5320u >> (4 * e_t)) & 0xF;  // copies: 2, 3, 5 bytes
+            const bool is_l = e_t == 0, is_c1 = e_t == 1, is_c2 = e_t == 2;
+            const uint32_t cx_olen = is_c1 ? c1_olen : c_olen;
+            e_len = is_l ? l_olen : cx_olen;  // garbage lengths are clamped below
+            const uint32_t c24 = is_c2 ? c2b : eb4;
+            const uint32_t cx_info = is_c1 ? c1b : c24;
+            e_info = is_l ? l_info : cx_info;
+            e_size = is_l ? l_size : c_size;
+        }
         // exclusive prefix sums of compressed sizes and output lengths over
         // the batch (64-bit safe: garbage past E is zeroed)
         const bool live = lane < E;
         uint32_t tot_in, tot_out;
-        const uint32_t in_off = wave_excl_scan32(live ? e_size : 0, &tot_in);  // E <= 32
-        const uint32_t out_off = wave_excl_scan32(live ? e_len : 0, &tot_out);
+        const uint32_t in_off = wave_excl_scan(live ? e_size : 0, lane, &tot_in);
+        const uint32_t out_off = wave_excl_scan(live ? e_len : 0, lane, &tot_out);
         // validity in stream order: stop at the first element that runs past the
         // unit (truncated / overrun), reaches before the stream start, or needs
         // an earlier unit's bytes (pass 1: DEFER); an element running past the

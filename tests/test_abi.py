@@ -178,6 +178,8 @@ def test_asm_memory_ops_drained(tmp_path, obj):
     import check_asm_waits
     assert "global_load_lds" in dis or obj.endswith("_d.o")  # the checker sees the compress kernels' DMA
     assert check_asm_waits.check(dis) == []
+    if obj.endswith("_d.o"):  # K4's element-start bitmap: clear, or, read in that order
+        assert check_asm_waits.check_k4_bitmap(dis) == []
     csrc = os.path.join(ROOT, "lightweight-snappy_amd", "csrc")
     for f in sorted(os.listdir(csrc)):
         if f.endswith(".hip"):

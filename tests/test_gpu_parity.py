@@ -1017,3 +1017,19 @@ def test_decompress_file_bogus_length():
     with pytest.raises(snappy_amd.SnappyError) as ei:
         snappy_amd.decompress(bogus)
     assert ei.value.code == snappy_amd.ERR_TRUNCATED
+
+
+def test_host_buffer_pipelined_chunks():
+    """snappy_compress_buffer of more than one 64 MiB chunk runs as a pipeline
+    of chunk lanes (csrc/snappy_device.hip host_compress_pipelined): the
+    stream equals the one-shot reference stream for sizes around the chunk
+    and lane-reuse boundaries (5 chunks > 4 lanes), and round-trips."""
+    M = 1 << 20
+    for n, kind, seed in (((64 << 20) + 1, "T", 81), ((128 << 20) + 65536 * 3 + 7, "T", 82),
+                          (300 * M + 12345, "T", 83), (70 * M, "R", 84)):
+        a = datagen.make(kind, n, seed)
+        got = snappy_amd.compress(a.tobytes())
+        want = oracle.compress_parallel(a, threads=16).tobytes()
+        assert len(got) == len(want) and got == want, (kind, n)
+        assert snappy_amd.decompress(got) == a.tobytes(), (kind, n)
+        progress(f"pipelined host compress {kind} {n}: ok")

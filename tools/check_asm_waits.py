@@ -84,6 +84,31 @@ def check(text):
     return bad
 
 
+def check_k4_bitmap(text, at=784):
+    """[(kernel, message)] unless every K4 bitmap `ds_or_b32 ... offset:<at>`
+    (kK4MapAt: a batch's element-start bitmap) lies between its clear (the
+    previous access at that offset is a ds_write_b32) and its read (the next one
+    is a ds_read_b32): the compiler barriers in k4_body keep that order, and a
+    reorder would read a half-built bitmap."""
+    bad, found = [], 0
+    tag = f"offset:{at}"
+    for name, (base, ins) in kernels(text).items():
+        if "k4_decompress" not in name:
+            continue
+        acc = [(i, op.split()[0]) for i, (_, op, _) in enumerate(ins) if op.startswith("ds_") and tag in op]
+        for k, (i, mn) in enumerate(acc):
+            if mn != "ds_or_b32":
+                continue
+            found += 1
+            prev = acc[k - 1][1] if k else None
+            nxt = acc[k + 1][1] if k + 1 < len(acc) else None
+            if prev != "ds_write_b32" or nxt != "ds_read_b32":
+                bad.append((name, f"bitmap ds_or at {ins[i][0]:#x}: previous {prev}, next {nxt}"))
+    if not found:
+        bad.append(("k4", "no K4 bitmap ds_or_b32 found"))
+    return bad
+
+
 _ASM = re.compile(r"\basm\s+(?:volatile\s*)?\(", re.S)
 _LOAD = re.compile(r"\b(ds_read\w*|global_load\w*|buffer_load\w*|flat_load\w*|s_load\w*|s_buffer_load\w*)\b")
 

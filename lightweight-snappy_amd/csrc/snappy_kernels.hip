@@ -718,12 +718,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     // lgkmcnt(0), so `ent`/`ent_t` are complete when the compiler reads them.
     // m0 (the writelane lane select) is saved and restored.  The loop always
     // advances p (a match by >= 4, a missing round by nk >= 1), so it ends.
-#if !defined(SNAPPY_K1R_STATS) && !defined(SNAPPY_K1R_LSTAMPS) && !defined(SNAPPY_K1R_CXX_ROUNDS) && \
-    !defined(SNAPPY_K1R_PACKED3)
+#if defined(SNAPPY_K1R_ASM_V) && !defined(SNAPPY_K1R_STATS) && !defined(SNAPPY_K1R_LSTAMPS) && \
+    !defined(SNAPPY_K1R_CXX_ROUNDS) && !defined(SNAPPY_K1R_PACKED3)
 #define K1R_ASM_ROUNDS 1
-#ifndef SNAPPY_K1R_ASM_V
-#define SNAPPY_K1R_ASM_V 2
-#endif
 #else
 #define K1R_ASM_ROUNDS 0
 #endif

@@ -2551,6 +2551,72 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             // element k: kop = output start | literal flag (bit 31); kinfo = the
             // copy offset, or for a literal its window address (slot base + data
             // start) + 2^31, so that kinfo + (o - kop) is byte o's window address
+#ifndef SNAPPY_K4_PASS_V
+#define SNAPPY_K4_PASS_V 2  // 1: round 3's byte pass in pass 1 too
+#endif
+            if constexpr (!BACK && SNAPPY_K4_PASS_V == 2) {
+            // element k: kop = output start | literal flag (bit 31); kd such that
+            // x = o + kd is byte o's window address (a literal: slot base + data
+            // start - output start) or its copy source (a copy: -offset)
+            const uint32_t kop = e_op | (e_t == 0 ? 0x80000000u : 0u);
+            const uint32_t kd = e_t == 0 ? 256 * ws + e_lsrc - e_op : 0u - e_info;
+            uint32_t cb = 0;  // elements starting before the pass
+            uint32_t o = op + lane;
+            // pass P: byte lane l writes output byte o = P + l
+            for (uint32_t P = op, i = 0; P < op_end; P += 64, i++, o += 64) {
+                const uint64_t sm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(bm, 2 * i + 1) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane(bm, 2 * i);
+                // the byte's element: cb - 1 + the starts in [P, P + l] (the first
+                // pass starts with one, so it is never -1)
+                const uint64_t sm1 = sm >> 1;
+                const uint32_t id = __builtin_amdgcn_mbcnt_hi(
+                    (uint32_t)(sm1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm1, cb - 1 + (uint32_t)(sm & 1)));
+                cb += (uint32_t)__builtin_popcountll(sm);
+                const uint32_t f_op = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)kop);
+                const uint32_t x = o + (uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)kd);
+                const bool lit = (int32_t)f_op < 0;
+                const bool pend = o < op_end;
+                // a copy's source below lo is only in HBM (a far copy never
+                // overlaps: off > ring - 64 > len), its load first, into its own register
+                bool far = pend && !lit && x < lo;
+                uint32_t fv = 0;
+#ifndef SNAPPY_K4_NOFAR
+                if (far) fv = dst[x];
+#endif
+                // literal byte: the window's LDS copy (3 slots of 256 bytes), read
+                // by every lane (no exec change): a copy lane's address is clamped
+                const uint32_t a2 = x - 768;
+                const uint32_t a = x < a2 ? x : a2;
+                const uint32_t lb = wb[a < 783 ? a : 783];
+                uint32_t src = x;
+                if (pend && !lit && !far && x >= f_op) {
+                    // overlapping copy (off < len <= 64): source byte d mod off
+                    const uint32_t off = o - x, d = o - f_op;
+                    const float r = __builtin_amdgcn_rcpf((float)off);
+                    const uint32_t qd = (uint32_t)((float)d * r + 0.0001f);
+                    src = f_op - off + (d - qd * off);
+                }
+                // a byte whose source lies in this pass reads garbage from the ring,
+                // replaced below; two selects over values every lane loaded (kept as
+                // bytes: see the round-3 pass below)
+                const uint8_t rv = ob[src & M];
+                const uint8_t lr = lit ? (uint8_t)lb : rv;
+                uint32_t val = far ? fv : (uint32_t)lr;
+                const uint64_t ipm = __ballot(pend && !lit && !far && src >= P);
+                if (__builtin_expect(ipm != 0, 0)) {
+                    // out[op+j] = out[op-off + j mod off] (:273-280) with the source in
+                    // this pass: lane src - P (a lower lane) holds it; pointer jumping
+                    uint32_t rt = ((ipm >> lane) & 1) ? src - P : lane;
+                    for (;;) {
+                        const uint32_t r2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rt << 2), (int)rt);
+                        if (!__ballot(r2 != rt)) break;
+                        rt = r2;
+                    }
+                    val = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rt << 2), (int)val);
+                }
+                ob[pend ? (o & M) : kK4Ring] = (uint8_t)val;
+            }
+            } else {
             const uint32_t kop = e_op | (e_t == 0 ? 0x80000000u : 0u);
             const uint32_t kinfo = e_t == 0 ? (256 * ws + e_lsrc) ^ 0x80000000u : e_info;
             uint32_t cb = 0;  // elements starting before the pass
@@ -2636,6 +2702,7 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 n_sub++;
 #endif
             }
+                    }
         }
         K4STAMP(td);
 #ifdef SNAPPY_K4_STATS

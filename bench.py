@@ -103,6 +103,8 @@ def parse(argv=None):
     ap.add_argument("--no-assemble", action="store_true", help="N > 1: skip the end-to-end loop with C2")
     ap.add_argument("--c3", action="store_true", help="N > 1: also time C3, the all-gather of the decoded shards")
     ap.add_argument("--e2e-steps", type=int, default=3, help="N > 1: steps of the end-to-end loop")
+    ap.add_argument("--overlap", action="store_true",
+                    help="decode piece k on a second stream while piece k + 1 compresses")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-e2e", action="store_true", help="skip the PCIe-inclusive host API samples")
     ap.add_argument("--no-sub", action="store_true", help="N = 1: skip the sub-results of the other configs")
@@ -484,6 +486,8 @@ class Job:
         self.header_value = total_in if layout == snappy_amd.SINGLE else n
         self.pre_clen = None
         self.g_offs = None
+        self.dcodec = self.dstream = None  # --overlap: the decode codec and its stream
+        self.last_dec = codec  # the codec of the last decode (its status is the one to read)
         if self.decode_only:  # the stream and its block index exist before the timed region
             self.pre_clen = self.compress_all()
             self.g_offs = torch.cat([p.offs[:-1] + p.out_off for p in self.pieces] +
@@ -498,9 +502,41 @@ class Job:
             o += p.clen
         return o
 
+    def step_overlapped(self, c1=None) -> int:
+        """One compress + decompress step with the decode of piece k (on the
+        second codec's stream) running while piece k + 1 compresses: K4 is
+        issue-bound and K1r latency-bound, so their waves share the CUs.  Piece
+        k's compression waits for its previous decode (an event), so the next
+        step never overwrites a payload still being read."""
+        o = 0
+        for k, p in enumerate(self.pieces):
+            if self.dec_done[k] is not None:
+                torch.cuda.current_stream(self.dev).wait_event(self.dec_done[k])
+            p.out_off = o
+            p.clen = self.codec.compress_ptr_ex(self.x.data_ptr() + p.off, p.n, self.chunk, self.layout, p.flags,
+                                                self.header_value, self.out.data_ptr() + o, p.offs.data_ptr())
+            o += p.clen
+            # piece k is compressed (compress_ptr_ex synchronised its stream): decode it on stream B
+            self.dstream.wait_stream(torch.cuda.current_stream(self.dev))
+            self.dcodec.decompress_ptr_ex(self.out.data_ptr() + p.out_off, p.offs.data_ptr(), p.n, self.chunk,
+                                          self.layout, p.flags, self.header_value, self.back.data_ptr() + p.off,
+                                          check=False)
+            self.last_dec = self.dcodec
+            ev = torch.cuda.Event()
+            ev.record(self.dstream)
+            self.dec_done[k] = ev
+        if c1 is not None:
+            c1(o)
+        return o
+
+    def enable_overlap(self, dcodec, dstream) -> None:
+        self.dcodec, self.dstream = dcodec, dstream
+        self.dec_done = [None] * len(self.pieces)
+
     def decompress_all(self, base_ptr=None) -> None:
         """Decode every piece from the payload at base_ptr (default: this rank's own)."""
         base_ptr = self.out.data_ptr() if base_ptr is None else base_ptr
+        self.last_dec = self.codec
         if self.decode_only:
             self.codec.decompress_ptr_ex(base_ptr, self.g_offs.data_ptr(), self.n, self.chunk, self.layout,
                                          self.pieces[0].flags, self.header_value, self.back.data_ptr(), check=False)
@@ -510,7 +546,7 @@ class Job:
                                          p.flags, self.header_value, self.back.data_ptr() + p.off, check=False)
 
     def verify(self) -> bool:
-        st = self.codec.decompress_status()
+        st = self.last_dec.decompress_status()
         if st != 0:
             return False
         # in 1 GiB slices: torch.equal's temporaries stay small next to a 64 GiB shard
@@ -534,6 +570,8 @@ def timed_steps(job: Job, steps: int, warmup: int, world: int, c1=None):
         if job.decode_only:
             job.decompress_all()
             return job.pre_clen
+        if job.dcodec is not None:
+            return job.step_overlapped(c1)
         clen = job.compress_all()
         if c1 is not None:
             c1(clen)
@@ -552,6 +590,8 @@ def timed_steps(job: Job, steps: int, warmup: int, world: int, c1=None):
     for _ in range(steps):
         clen = step()
         a, b, c = job.codec.last_timings()
+        if job.dcodec is not None:
+            c = job.dcodec.last_timings()[2]
         k1.append(a), k3.append(b), k4.append(c)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -701,6 +741,13 @@ def main():
     codec.set_stream(stream.cuda_stream)
     t_setup = time.perf_counter()
     job = Job(args.workload, codec, dev, n, r_off, total_in, n_max, args.piece_bytes)
+    dcodec = None
+    if args.overlap and not decode_only:
+        dcodec = snappy_amd.Codec(dev.index)
+        dcodec.enable_timing(True)
+        dstream = torch.cuda.Stream(dev)
+        dcodec.set_stream(dstream.cuda_stream)
+        job.enable_overlap(dcodec, dstream)
     t_setup = time.perf_counter() - t_setup
     sizes_t = torch.zeros(world, dtype=torch.int64, device=cdev)
 
@@ -718,7 +765,7 @@ def main():
 
     elapsed, clen, k1, k3, k4 = timed_steps(job, args.steps, args.warmup, world if use_dist else 1,
                                             c1 if use_dist else None)
-    scratch_peak = codec.device_bytes()
+    scratch_peak = codec.device_bytes() + (dcodec.device_bytes() if dcodec else 0)
     torch_peak = torch.cuda.max_memory_allocated(dev)  # the buffers of the steps, before any check runs
     ok = job.verify()
     if use_dist:
@@ -780,7 +827,8 @@ def main():
                        "bytes_per_gpu": n, "total_bytes": total_in, "chunk": chunk,
                        "layout": "STREAMS" if layout else "SINGLE", "units_per_gpu": n_units,
                        "pieces_per_gpu": len(job.pieces), "launch_bytes": launch_bytes,
-                       "workload_name": args.workload, "parallelism": f"dp{world} (block shards)"},
+                       "workload_name": args.workload, "parallelism": f"dp{world} (block shards)",
+                       "overlap": bool(dcodec)},
             "roofline": rep["roofline"],
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
@@ -824,6 +872,8 @@ def main():
     if line is not None:
         print(json.dumps(line), flush=True)
     codec.close()
+    if dcodec:
+        dcodec.close()
     if use_dist:
         dist.destroy_process_group()
     if not ok:

@@ -30,6 +30,13 @@ for step in "$@"; do
             python3 bench.py --total-bytes 68719476736 --steps 2 --warmup 1 --no-cpu-baseline --no-host-e2e \
             > "$out/n1_64g_trace.log" 2>&1
         rc=$?; echo "prof64g rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
+    ovl)  # the default job with and without --overlap (decode of piece k during the compress of k + 1)
+        for o in "" "--overlap" "" "--overlap"; do
+            timeout -k 10 300 python -u bench.py --steps 4 --warmup 1 --no-sub --no-cpu-baseline --no-host-e2e $o \
+                >> "$out/ovl.json" 2>> "$out/ovl.err"
+            rc=$?; echo "ovl '$o' rc=$rc"; [ $rc -ne 0 ] && exit $rc
+        done
+        python3 -c "import json,sys; [print(d['config']['overlap'], d['ms_per_step'], d['value'], d['kernel_ms'], d['round_trip_ok']) for d in map(json.loads, [l for l in open(sys.argv[1]) if l.startswith('{')])]" "$out/ovl.json" ;;
     ab:*)  # ab:<variant,variant,...>:<kind>:<chunk>:<layout> -> tools/variant_bench.py, 1 GiB
         IFS=: read -r _ vs kind chunk layout <<< "$step"
         timeout -k 10 400 python -u tools/variant_bench.py ${vs//,/ } --kind $kind --n 1073741824 --chunk $chunk \

@@ -55,6 +55,7 @@ struct snappy_amd_ctx {
     bool serial_index = false;  // SNAPPY_AMD_OPT_SERIAL_INDEX
     uint32_t k1r_extra_lds = 0; // SNAPPY_AMD_OPT_K1R_EXTRA_LDS
     hipEvent_t ev[5] = {};
+    bool ev_compress = false, ev_decode = false;  // ev[0..2] / ev[3..4] recorded by a launch
     float k1_ms = 0, k3_ms = 0, k4_ms = 0;
 };
 
@@ -185,12 +186,14 @@ int snappy_amd_last_timings(snappy_amd_ctx *c, float *k1, float *k3, float *k4)
     if (!c) return SNAPPY_AMD_ERR_ARG;
     if (c->timing) {
         // resolve whatever the stream has recorded so far (waits for it)
+        // (only events a launch recorded: an elapsed time of an unrecorded event
+        // fails, and its error would stay pending for the thread's next check)
         (void)hipSetDevice(c->device);
-        if (hipEventSynchronize(c->ev[2]) == hipSuccess) {
+        if (c->ev_compress && hipEventSynchronize(c->ev[2]) == hipSuccess) {
             (void)hipEventElapsedTime(&c->k1_ms, c->ev[0], c->ev[1]);
             (void)hipEventElapsedTime(&c->k3_ms, c->ev[1], c->ev[2]);
         }
-        if (c->last_units && hipEventSynchronize(c->ev[4]) == hipSuccess)
+        if (c->ev_decode && c->last_units && hipEventSynchronize(c->ev[4]) == hipSuccess)
             (void)hipEventElapsedTime(&c->k4_ms, c->ev[3], c->ev[4]);
     }
     if (k1) *k1 = c->k1_ms;
@@ -248,6 +251,9 @@ static int compress_impl(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t
     if ((rc = grow(reinterpret_cast<void **>(&c->seg_off), &c->seg_off_cap, units * segs * 2 * sizeof(uint32_t))))
         return rc;
     const uint32_t hm = hdr_mode_of(layout, flags);
+    // launch errors are read with hipGetLastError: clear one a runtime call of
+    // the caller's (or of another context on this thread) left pending
+    (void)hipGetLastError();
     if (c->timing) (void)hipEventRecord(c->ev[0], c->stream);
     // units <= 32 KiB: the unit in 128 VGPRs; 65,536-byte blocks: its last 128
     // segments in a 128-VGPR ring fed by LDS-DMA (both 3 waves/SIMD).
@@ -270,7 +276,10 @@ static int compress_impl(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t
                        static_cast<const uint8_t *>(d_in), (uint64_t)n, unit, hm, header_value, c->tokens, tok_cap,
                        c->ntok, c->seg_off, segs, d_offsets, static_cast<uint8_t *>(d_out));
     HIP_OK(hipGetLastError());
-    if (c->timing) (void)hipEventRecord(c->ev[2], c->stream);
+    if (c->timing) {
+        (void)hipEventRecord(c->ev[2], c->stream);
+        c->ev_compress = true;
+    }
     if (out_len) {
         HIP_OK(hipMemcpyAsync(c->h_total, c->total, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
         HIP_OK(hipStreamSynchronize(c->stream));
@@ -315,6 +324,7 @@ static int decompress_launch(snappy_amd_ctx *c, const void *d_comp, const uint64
     // reach into earlier blocks (src/snappy_decompression.c:253-280, 345-363);
     // pass 1 decodes every self-contained block, pass 2 the others in order
     const uint32_t allow_back = layout == SNAPPY_AMD_SINGLE ? 1u : 0u;
+    (void)hipGetLastError();  // (a pending error that is not this launch's, as in compress_impl)
     if (c->timing) (void)hipEventRecord(c->ev[3], c->stream);
     if (allow_back) HIP_OK(hipMemsetAsync(c->status + units, 0, 2 * sizeof(int32_t), c->stream));
     const uint32_t hm = hdr_mode_of(layout, flags);
@@ -331,7 +341,10 @@ static int decompress_launch(snappy_amd_ctx *c, const void *d_comp, const uint64
                            c->status);
         HIP_OK(hipGetLastError());
     }
-    if (c->timing) (void)hipEventRecord(c->ev[4], c->stream);
+    if (c->timing) {
+        (void)hipEventRecord(c->ev[4], c->stream);
+        c->ev_decode = true;
+    }
     c->last_units = units;
     c->last_layout = layout;
     return SNAPPY_AMD_OK;
@@ -352,7 +365,7 @@ int snappy_amd_decompress_status(snappy_amd_ctx *c)
     }
     HIP_OK(hipMemcpyAsync(c->h_status, c->status, bytes, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
-    if (c->timing) (void)hipEventElapsedTime(&c->k4_ms, c->ev[3], c->ev[4]);
+    if (c->timing && c->ev_decode) (void)hipEventElapsedTime(&c->k4_ms, c->ev[3], c->ev[4]);
     for (size_t i = 0; i < c->last_units; i++) {
         // DEFER survives a STREAMS launch (no pass 2) only for a copy reaching
         // before the start of its own stream; after a SINGLE launch pass 2 ends
@@ -392,6 +405,7 @@ int snappy_amd_index_device(snappy_amd_ctx *c, const void *d_comp, size_t clen, 
 {
     if (!c || !d_comp || !d_offsets) return SNAPPY_AMD_ERR_ARG;
     HIP_OK(hipSetDevice(c->device));
+    (void)hipGetLastError();  // (a pending error that is not this launch's, as in compress_impl)
     const uint8_t *comp = static_cast<const uint8_t *>(d_comp);
     const bool serial = c->serial_index;
     if (!serial && clen >= 4 * (size_t)K5_CHUNK && (reinterpret_cast<uintptr_t>(d_comp) & 3)) {

@@ -265,6 +265,28 @@ def test_config3_64gib_full_stream(codec):
     torch.cuda.empty_cache()
 
 
+def test_timings_before_any_launch_leave_no_pending_error():
+    """A context that has timed nothing yet (bench.py --overlap's decode codec
+    before its first decode) reads its timings, then another context on the
+    same thread compresses and decodes: the launch-error checks must report
+    only their own launches' errors (round 4: an elapsed time of an unrecorded
+    event stayed pending and failed the next compress as a HIP error)."""
+    import torch
+    idle = snappy_amd.Codec(0)
+    idle.enable_timing(True)
+    assert idle.last_timings() == (0.0, 0.0, 0.0)
+    c = snappy_amd.Codec(0)
+    c.enable_timing(True)
+    a = datagen.make("T", 1 << 20, 5)
+    x = to_dev(a)
+    comp, offs = c.compress_tensor(x, chunk=32768, layout=snappy_amd.STREAMS)
+    idle.last_timings()
+    back = c.decompress_tensor(comp, offs, x.numel(), chunk=32768, layout=snappy_amd.STREAMS)
+    assert torch.equal(back, x)
+    k1, k3, k4 = c.last_timings()
+    assert k1 > 0 and k3 > 0 and k4 > 0
+
+
 def test_default_stream_ordering(codec):
     """A tensor written on torch's default stream (the legacy null stream, which
     the binding maps to the context's own stream) is compressed only after that
@@ -1017,6 +1039,20 @@ def test_decompress_file_bogus_length():
     with pytest.raises(snappy_amd.SnappyError) as ei:
         snappy_amd.decompress(bogus)
     assert ei.value.code == snappy_amd.ERR_TRUNCATED
+
+
+def test_host_buffer_sizes_to_one_chunk():
+    """snappy_compress_buffer / snappy_decompress_buffer at sizes from 8 MiB
+    up to one pipeline chunk (64 MiB), incl. odd ones: the one-shot stream
+    byte for byte, and the round trip."""
+    M = 1 << 20
+    for n, seed in ((8 * M - 1, 91), (8 * M, 92), (16 * M + 1, 93), (48 * M + 3, 94), (64 * M, 95)):
+        a = datagen.make("T", n, seed)
+        got = snappy_amd.compress(a.tobytes())
+        want = oracle.compress_parallel(a, threads=16).tobytes()
+        assert got == want, n
+        assert snappy_amd.decompress(got) == a.tobytes(), n
+        progress(f"host buffer {n}: ok")
 
 
 def test_host_buffer_pipelined_chunks():

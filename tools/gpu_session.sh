@@ -76,6 +76,16 @@ for step in "$@"; do
         K1R_CHUNK=$chunk K1R_ROUNDS=$rnds timeout -k 10 200 python -u tools/k1r_stamps.py 268435456 "" $v \
             > "$out/k1s_${v}_$chunk.log" 2>&1
         rc=$?; echo "k1s $v rc=$rc"; cat "$out/k1s_${v}_$chunk.log"; [ $rc -ne 0 ] && exit $rc ;;
+    pageable)  # host-buffer staging floor: runtime pageable copies vs threaded memcpy into pinned memory
+        timeout -k 10 200 python -u tools/pageable_probe.py > "$out/pageable_probe.log" 2>&1
+        rc=$?; echo "pageable rc=$rc"; cat "$out/pageable_probe.log"; [ $rc -ne 0 ] && exit $rc ;;
+    ovl16)  # --overlap A/B at 16 GiB (two pieces)
+        for o in "" "--overlap" "" "--overlap"; do
+            timeout -k 10 300 python -u bench.py --total-bytes 17179869184 --steps 4 --warmup 1 --no-sub --no-cpu-baseline \
+                --no-host-e2e $o >> "$out/ovl16.json" 2>> "$out/ovl16.err"
+            rc=$?; echo "ovl16 '$o' rc=$rc"; [ $rc -ne 0 ] && exit $rc
+        done
+        python3 -c "import json,sys; [print(d['config']['overlap'], d['ms_per_step'], d['value'], d['kernel_ms'], d['round_trip_ok']) for d in map(json.loads, [l for l in open(sys.argv[1]) if l.startswith('{')])]" "$out/ovl16.json" ;;
     io)  # host I/O floor (tools/io_probe.py, no GPU) and the FILE* API with SNAPPY_AMD_IO_TRACE phase times
         timeout -k 10 200 python -u tools/io_probe.py 4 > "$out/io_probe.log" 2>&1
         rc=$?; echo "io_probe rc=$rc"; cat "$out/io_probe.log"; [ $rc -ne 0 ] && exit $rc

@@ -269,7 +269,10 @@ static int compress_impl(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t
                            tok_cap, c->ntok, c->sizes, c->seg_off, segs);
     HIP_OK(hipGetLastError());
     if (c->timing) (void)hipEventRecord(c->ev[1], c->stream);
-    hipLaunchKernelGGL(k3_scan, dim3(1), dim3(1024), 0, c->stream, c->sizes, (uint64_t)units, d_offsets, c->total);
+    if (units <= SNAPPY_K3_WAVE_MAX)
+        hipLaunchKernelGGL(k3_scan_wave, dim3(1), dim3(64), 0, c->stream, c->sizes, (uint64_t)units, d_offsets, c->total);
+    else
+        hipLaunchKernelGGL(k3_scan, dim3(1), dim3(1024), 0, c->stream, c->sizes, (uint64_t)units, d_offsets, c->total);
     // K1r wrote the sizes and segment offsets; K2: a few waves per unit, each taking
     // every SNAPPY_K2_WAVES-th segment (text fills ~12 segments of 32 KiB units)
     hipLaunchKernelGGL(k2_emit_units, dim3((uint32_t)units, segs < SNAPPY_K2_WAVES ? segs : SNAPPY_K2_WAVES), dim3(64), 0, c->stream,
@@ -817,15 +820,26 @@ int dec_stage_init(DecStage &d)
 // own streams, scratch and pinned staging.  The pool's lock is held only to
 // take or return a context.  The device is the calling thread's
 // (snappy_amd_host_set_device), else SNAPPY_AMD_DEVICE (read once), else 0.
-constexpr int kPipeLanes = 4;                    // host-buffer compress: chunks in flight
-constexpr size_t kPipeChunk = (size_t)64 << 20;  // ... of this many bytes (1,024 blocks)
+constexpr int kPipeLanesMax = 16;
+// host-buffer compress: chunks in flight (SNAPPY_AMD_PIPE_LANES, default 4) of
+// SNAPPY_AMD_PIPE_CHUNK_MB MiB each (a multiple of the 65,536-byte block; default 64 = 1,024 blocks)
+int pipe_lanes()
+{
+    static const int l = std::min(kPipeLanesMax, env_threads("SNAPPY_AMD_PIPE_LANES", 4));
+    return l;
+}
+size_t pipe_chunk()
+{
+    static const size_t c = (size_t)std::max(1, std::min(4096, env_threads("SNAPPY_AMD_PIPE_CHUNK_MB", 64))) << 20;
+    return c;
+}
 
 struct HostCtx {
     int device = 0;
     snappy_amd_ctx *c = nullptr;           // host-buffer path and the FILE* decoder
     StreamSlot slots[2];                   // the FILE* compressor's two pipeline slots
     DecStage dec;                          // the FILE* decoder's pinned staging
-    snappy_amd_ctx *pipe[kPipeLanes] = {}; // the host-buffer compressor's chunk lanes
+    snappy_amd_ctx *pipe[kPipeLanesMax] = {}; // the host-buffer compressor's chunk lanes
 };
 
 void host_free(HostCtx *h)
@@ -833,7 +847,8 @@ void host_free(HostCtx *h)
     if (!h) return;
     (void)hipSetDevice(h->device);
     for (auto &s : h->slots) slot_free(s);
-    for (auto *p : h->pipe) snappy_amd_destroy(p);
+    for (auto *p : h->pipe)
+        if (p != h->c) snappy_amd_destroy(p);
     dec_stage_free(h->dec);
     snappy_amd_destroy(h->c);
     delete h;
@@ -956,7 +971,7 @@ size_t snappy_amd_host_pool_size(void)
 
 // A host buffer of more than one 64 MiB chunk: each chunk (a multiple of the
 // 65,536-byte block, so the bytes are those of the one-shot stream; chunks
-// after the first without the preamble) goes to one of kPipeLanes contexts of
+// after the first without the preamble) goes to one of pipe_lanes() contexts of
 // its own stream -- H2D, K1r/K3/K2, the compressed size back to pinned memory
 // -- so the chunks' copies and kernels overlap and their kernels fill the chip
 // together (one 64 MiB chunk is 1,024 blocks on 3,072 wave slots); the
@@ -965,10 +980,16 @@ size_t snappy_amd_host_pool_size(void)
 int host_compress_pipelined(HostCtx &h, const uint8_t *in, size_t n, uint64_t header_value, uint8_t *out,
                             size_t cap, size_t *out_len)
 {
+    const size_t kPipeChunk = pipe_chunk();
     const size_t nch = (n + kPipeChunk - 1) / kPipeChunk;
-    const int lanes = (int)std::min<size_t>((size_t)kPipeLanes, nch);
+    const int lanes = (int)std::min<size_t>((size_t)pipe_lanes(), nch);
     int rc;
-    for (int i = 0; i < lanes; i++)
+    // lane 0 is the host context's own: every stream takes one of the process's
+    // hardware queues (GPU_MAX_HW_QUEUES, 4 by default), and a lane that shares
+    // one with another stream waits behind that stream's work (a fourth lane of
+    // its own queued its K1r behind another lane's K2: profiles/r04e_host_trace_*)
+    h.pipe[0] = h.c;
+    for (int i = 1; i < lanes; i++)
         if (!h.pipe[i] && (rc = snappy_amd_create(h.device, &h.pipe[i]))) {
             h.pipe[i] = nullptr;
             return rc;
@@ -1014,7 +1035,7 @@ int snappy_amd_host_compress(const uint8_t *in, size_t n, uint64_t header_value,
     if (n == 0) return SNAPPY_AMD_OK;
     Lease h(host_device());
     if (h.rc()) return h.rc();
-    if (n > kPipeChunk) return host_compress_pipelined(*h, in, n, header_value, out, cap, out_len);
+    if (n > pipe_chunk()) return host_compress_pipelined(*h, in, n, header_value, out, cap, out_len);
     size_t len = 0;
     int rc = host_compress_stage(*h, in, n, 0, header_value, &len);
     if (rc) return rc;

@@ -51,6 +51,10 @@ __global__ void k2_emit_units(const uint8_t *__restrict__ in, uint64_t n, uint32
 
 __global__ void k3_scan(const uint32_t *__restrict__ sizes, uint64_t count, uint64_t *__restrict__ offsets,
                         uint64_t *__restrict__ total);
+// one-wave K3 for launches of at most SNAPPY_K3_WAVE_MAX units
+__global__ void k3_scan_wave(const uint32_t *__restrict__ sizes, uint64_t count, uint64_t *__restrict__ offsets,
+                             uint64_t *__restrict__ total);
+#define SNAPPY_K3_WAVE_MAX 8192u
 // K4: comp is 4-byte aligned, the stream starts at comp + bias (bias < 4).
 // K4 pass 1: every unit; allow_back = 1 for SINGLE-layout streams (straddling
 // elements and copies into earlier blocks are legal: such units end with

@@ -1640,6 +1640,41 @@ __global__ __launch_bounds__(1024) void k3_scan(const uint32_t *__restrict__ siz
         *total = carry;
     }
 }
+
+// The same scan in one wave (lane l scans sizes 8 l .. 8 l + 7 of each group of
+// 512), for launches of few units: a 1,024-thread workgroup needs 16 free wave
+// slots on one CU, which it does not get while another stream's match finder
+// fills every SIMD (the host-buffer pipeline's chunk lanes: a K3 of 1,024
+// blocks waited 1.06 ms for a CU, profiles/r04e_host_trace_*); one wave starts
+// on the first free slot.
+__global__ __launch_bounds__(64) void k3_scan_wave(const uint32_t *__restrict__ sizes, uint64_t count,
+                                                  uint64_t *__restrict__ offsets, uint64_t *__restrict__ total)
+{
+    const uint32_t lane = threadIdx.x;
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < count; b += 64 * kScanPer) {
+        uint32_t v[kScanPer], s = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kScanPer; k++) {
+            const uint64_t i = b + kScanPer * lane + k;
+            v[k] = i < count ? sizes[i] : 0u;
+            s += v[k];
+        }
+        uint32_t tot;
+        uint32_t run = wave_excl_scan(s, lane, &tot);
+#pragma unroll
+        for (uint32_t k = 0; k < kScanPer; k++) {
+            const uint64_t i = b + kScanPer * lane + k;
+            if (i < count) offsets[i] = carry + run;
+            run += v[k];
+        }
+        carry += tot;
+    }
+    if (lane == 0) {
+        offsets[count] = carry;
+        *total = carry;
+    }
+}
 #endif
 
 // ---------------------------------------------------------------------------

@@ -86,6 +86,16 @@ for step in "$@"; do
             rc=$?; echo "ovl16 '$o' rc=$rc"; [ $rc -ne 0 ] && exit $rc
         done
         python3 -c "import json,sys; [print(d['config']['overlap'], d['ms_per_step'], d['value'], d['kernel_ms'], d['round_trip_ok']) for d in map(json.loads, [l for l in open(sys.argv[1]) if l.startswith('{')])]" "$out/ovl16.json" ;;
+    hostpipe)  # host-buffer compress pipeline: lanes x chunk MiB sweep (tools/host_e2e.py, text 256 MiB)
+        for lc in 4:64 3:64 4:48 5:48 6:32 4:64; do
+            SNAPPY_AMD_PIPE_LANES=${lc%%:*} SNAPPY_AMD_PIPE_CHUNK_MB=${lc##*:} timeout -k 10 120 \
+                python -u tools/host_e2e.py 268435456 T > "$out/hostpipe_$lc.log" 2>&1
+            rc=$?; echo "hostpipe $lc rc=$rc: $(grep -h '^T' "$out/hostpipe_$lc.log")"; [ $rc -ne 0 ] && exit $rc
+        done ;;
+    hosttrace)  # kernel + memory-copy trace of the host-buffer API (timeline of the pipeline)
+        timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$out/hosttrace" -o run \
+            --output-format csv -- python3 tools/host_e2e.py 268435456 T > "$out/hosttrace.log" 2>&1
+        rc=$?; echo "hosttrace rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
     io)  # host I/O floor (tools/io_probe.py, no GPU) and the FILE* API with SNAPPY_AMD_IO_TRACE phase times
         timeout -k 10 200 python -u tools/io_probe.py 4 > "$out/io_probe.log" 2>&1
         rc=$?; echo "io_probe rc=$rc"; cat "$out/io_probe.log"; [ $rc -ne 0 ] && exit $rc

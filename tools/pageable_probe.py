@@ -58,3 +58,23 @@ for th in (1, 2, 4, 8, 16):
     r_in = best(lambda: par_copy(pin.data_ptr(), page.ctypes.data, th))
     r_out = best(lambda: par_copy(page2.ctypes.data, pin.data_ptr(), th))
     print(f"memcpy {th:2d} threads: pageable->pinned {r_in:6.1f} GB/s  pinned->pageable {r_out:6.1f} GB/s", flush=True)
+# sizes and offsets that are not multiples of 4 KiB (a compressed stream's length):
+# does the runtime still take the DMA path?
+for off, m in ((0, N - 3), (0, 145000001), (1, 145000000), (0, 145000000 - 145000000 % 4096)):
+    src = pt[off:off + m]
+    dst = dev[:m]
+    t = float("inf")
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dst.copy_(src)
+        torch.cuda.synchronize()
+        t = min(t, time.perf_counter() - t0)
+    t2 = float("inf")
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pt2[off:off + m].copy_(dev[:m])
+        torch.cuda.synchronize()
+        t2 = min(t2, time.perf_counter() - t0)
+    print(f"pageable offset {off} size {m}: h2d {m / t / 1e9:6.1f} GB/s  d2h {m / t2 / 1e9:6.1f} GB/s", flush=True)

@@ -92,6 +92,16 @@ for step in "$@"; do
                 python -u tools/host_e2e.py 268435456 T > "$out/hostpipe_$lc.log" 2>&1
             rc=$?; echo "hostpipe $lc rc=$rc: $(grep -h '^T' "$out/hostpipe_$lc.log")"; [ $rc -ne 0 ] && exit $rc
         done ;;
+    hostab:*)  # hostab:<variant,...> -> tools/host_e2e.py (text 256 MiB) per library variant, twice, interleaved
+        vs=${step#hostab:}
+        for r in 1 2; do for v in ${vs//,/ }; do
+            lib=""; [ "$v" != default ] && lib=$PWD/lightweight-snappy_amd/variants/libsnappy_amd_$v.so
+            SNAPPY_AMD_LIB=$lib timeout -k 10 120 python -u tools/host_e2e.py 268435456 T > "$out/hostab_${v}_$r.log" 2>&1
+            rc=$?; echo "hostab $v rc=$rc: $(grep -h '^T' "$out/hostab_${v}_$r.log")"; [ $rc -ne 0 ] && exit $rc
+        done; done ;;
+    copypath)  # which copy path (DMA engines or blit kernels) pageable copies take per stream (tools/micro/copy_path.hip)
+        timeout -k 10 120 tools/micro/copy_path > "$out/copy_path.log" 2>&1
+        rc=$?; echo "copypath rc=$rc"; cat "$out/copy_path.log"; [ $rc -ne 0 ] && exit $rc ;;
     hosttrace)  # kernel + memory-copy trace of the host-buffer API (timeline of the pipeline)
         timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$out/hosttrace" -o run \
             --output-format csv -- python3 tools/host_e2e.py 268435456 T > "$out/hosttrace.log" 2>&1

@@ -2086,23 +2086,32 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             ex0 = ax0;
             eb4 = ab4;
             E = ea;
-            // half B when its 64 positions and their 5 bytes stay in the valid
-            // window (bytes [0, 512) from B: o + xa + 63 + 5 < 512)
+            // more halves where the previous half's chain exits, while its 64
+            // positions and their 5 bytes stay in the valid window (bytes [0, 512)
+            // from B: hpos + 63 + 5 < 512) and lanes are free; elements past lane 63
+            // are dropped (the batch is a prefix of the element sequence, and the
+            // next batch starts after its last element).  Lanes >= E take the new
+            // half's element lane - E.  A/B on 1 GiB, outputs identical
+            // (profiles/r04a_ab_k4_*, r04k_ab_k4_*): K4 per GiB of 32 KiB text
+            // streams 3.11 / 2.65-2.69 / 2.51 ms with 1 / 2 / 3 halves, 64 KiB
+            // blocks 3.36 / 2.85-2.90 / 2.69-2.74
 #ifndef SNAPPY_K4_HALVES
-#define SNAPPY_K4_HALVES 2  // 1: one 64-position half per batch (round 3's batch size)
+#define SNAPPY_K4_HALVES 3
 #endif
-            if (SNAPPY_K4_HALVES > 1 && o + xa <= 440) {
+            uint32_t hpos = o + xa;
+#pragma unroll
+            for (int hh = 1; hh < SNAPPY_K4_HALVES; hh++) {
+                if (!(E < 64 && hpos <= 440)) break;
                 uint32_t bx0, bb4, eb, xb;
-                parse_half(o + xa, bx0, bb4, eb, xb);
-                (void)xb;
-                // lanes >= ea take B's element lane - ea
-                const int sa = (int)(4 * (lane - ea));
+                parse_half(hpos, bx0, bb4, eb, xb);
+                const int sa = (int)(4 * (lane - E));
                 const uint32_t sx0 = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)bx0);
                 const uint32_t sb4 = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)bb4);
-                const bool fa = lane < ea;
-                ex0 = fa ? ax0 : sx0;
-                eb4 = fa ? ab4 : sb4;
-                E = ea + eb;
+                const bool fa = lane < E;
+                ex0 = fa ? ex0 : sx0;
+                eb4 = fa ? eb4 : sb4;
+                E = E + eb < 64 ? E + eb : 64;
+                hpos += xb;
             }
         }
         // lane k < E holds element k of the batch; lanes >= E hold garbage,

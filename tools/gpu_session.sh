@@ -102,6 +102,16 @@ for step in "$@"; do
     copypath)  # which copy path (DMA engines or blit kernels) pageable copies take per stream (tools/micro/copy_path.hip)
         timeout -k 10 120 tools/micro/copy_path > "$out/copy_path.log" 2>&1
         rc=$?; echo "copypath rc=$rc"; cat "$out/copy_path.log"; [ $rc -ne 0 ] && exit $rc ;;
+    hostinbench)  # the bench line's host_end_to_end after a 1 GiB and after the 64 GiB job (no sub-results, no CPU baselines)
+        for tb in 1073741824 68719476736; do
+            timeout -k 10 400 python -u bench.py --total-bytes $tb --steps 2 --warmup 1 --no-sub --no-cpu-baseline \
+                > "$out/hostinbench_$tb.json" 2> "$out/hostinbench_$tb.err"
+            rc=$?; echo "hostinbench $tb rc=$rc: $(python3 -c "import json,sys; print(json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1])['host_end_to_end'])" "$out/hostinbench_$tb.json")"
+            [ $rc -ne 0 ] && exit $rc
+        done
+        timeout -k 10 500 rocprofv3 --kernel-trace --memory-copy-trace -d "$out/hostinbench_trace" -o run --output-format csv -- \
+            python3 bench.py --steps 1 --warmup 1 --no-sub --no-cpu-baseline > "$out/hostinbench_trace.log" 2>&1
+        rc=$?; echo "hostinbench trace rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
     hosttrace)  # kernel + memory-copy trace of the host-buffer API (timeline of the pipeline)
         timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$out/hosttrace" -o run \
             --output-format csv -- python3 tools/host_e2e.py 268435456 T > "$out/hosttrace.log" 2>&1

@@ -468,6 +468,24 @@ int snappy_amd_index_device(snappy_amd_ctx *c, const void *d_comp, size_t clen, 
 // reads chunk k+1.  Chunk 0 carries the varint(header_value) preamble, the
 // others are compressed with it suppressed.
 namespace {
+// A pipeline context's own stream at high priority: high-priority streams take
+// hardware queues of their own, where default-priority streams share the
+// process's few (GPU_MAX_HW_QUEUES, 4 by default) with the caller's streams,
+// and a stream sharing a queue waits behind the other's work (in bench.py's
+// process, next to torch's streams, two host-pipeline lanes each shared a
+// queue with another and the pipeline ran two chunks at a time: 256 MiB of
+// text 21.9 -> 28.9 GB/s, profiles/r04n_*).  A failure keeps the stream.
+void high_priority_stream(snappy_amd_ctx *c)
+{
+    int lo = 0, hi = 0;
+    hipStream_t st = nullptr;
+    if (c->stream != c->own || hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&st, hipStreamDefault, hi) != hipSuccess)
+        return;
+    (void)hipStreamDestroy(c->own);
+    c->own = c->stream = st;
+}
+
 struct StreamSlot {
     snappy_amd_ctx *c = nullptr;
     uint8_t *h_in = nullptr, *h_out = nullptr;
@@ -990,9 +1008,12 @@ int host_compress_pipelined(HostCtx &h, const uint8_t *in, size_t n, uint64_t he
     // its own queued its K1r behind another lane's K2: profiles/r04e_host_trace_*)
     h.pipe[0] = h.c;
     for (int i = 1; i < lanes; i++)
-        if (!h.pipe[i] && (rc = snappy_amd_create(h.device, &h.pipe[i]))) {
-            h.pipe[i] = nullptr;
-            return rc;
+        if (!h.pipe[i]) {
+            if ((rc = snappy_amd_create(h.device, &h.pipe[i]))) {
+                h.pipe[i] = nullptr;
+                return rc;
+            }
+            high_priority_stream(h.pipe[i]);
         }
     size_t off = 0;  // compressed bytes placed so far
     auto drain = [&](size_t k) -> int {

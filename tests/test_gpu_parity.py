@@ -380,6 +380,41 @@ def test_parallel_index_chains_that_never_converge(codec):
         assert back.cpu().numpy().tobytes() == want
 
 
+def test_decode_dense_short_elements(codec):
+    """K4 batches of up to three 64-position halves merge at most 64 elements and
+    drop the rest (the next batch starts after the last kept one): a stream of
+    2- and 3-byte elements -- 1-byte literals, copy-1 of 4-11 bytes and copy-2 of
+    1-3 bytes at offsets 1-40 -- fills 64 lanes in every batch and puts most copy
+    sources inside the same 64-byte pass.  Decoded as one SINGLE stream (K5p index
+    + K4) and as the host API does it, both equal to the oracle's decode."""
+    import torch
+    from golden_inputs import SplitMix64
+    rng = SplitMix64(2024)
+    ops, total = [], 0
+    while total < (3 << 20):
+        r = rng.below(10)
+        if r < 4 or total < 64:
+            ops.append(["lit", 1, rng.below(1 << 30)])
+            total += 1
+        elif r < 8:
+            ln = 4 + rng.below(8)
+            ops.append(["copy", ln, 1 + rng.below(min(40, total)), 1])
+            total += ln
+        else:
+            ln = 1 + rng.below(3)
+            ops.append(["copy", ln, 1 + rng.below(min(40, total)), 2])
+            total += ln
+    stream = build_stream(ops)
+    want = oracle.decompress(stream)
+    assert len(want) == total
+    assert snappy_amd.decompress(stream) == want
+    d = torch.from_numpy(np.frombuffer(stream, dtype=np.uint8).copy()).cuda()
+    n, offs = codec.index_tensor(d)  # K5p (chunk-parallel index)
+    assert n == total
+    back = codec.decompress_tensor(d, offs, total, layout=snappy_amd.SINGLE)
+    assert back.cpu().numpy().tobytes() == want
+
+
 def test_parallel_index_errors_match_serial(codec):
     import torch
     a = datagen.make("T", 6 << 20, 33)

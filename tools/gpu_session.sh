@@ -112,6 +112,13 @@ for step in "$@"; do
         timeout -k 10 500 rocprofv3 --kernel-trace --memory-copy-trace -d "$out/hostinbench_trace" -o run --output-format csv -- \
             python3 bench.py --steps 1 --warmup 1 --no-sub --no-cpu-baseline > "$out/hostinbench_trace.log" 2>&1
         rc=$?; echo "hostinbench trace rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
+    hostenv)  # host_end_to_end inside a 1 GiB bench run: as is, with high-priority lane streams, with 8 hardware queues
+        for e in "X=1" "SNAPPY_AMD_PIPE_PRIO=1" "GPU_MAX_HW_QUEUES=8"; do
+            env $e timeout -k 10 300 python -u bench.py --total-bytes 1073741824 --steps 2 --warmup 1 --no-sub --no-cpu-baseline \
+                > "$out/hostenv_$e.json" 2> "$out/hostenv_$e.err"
+            rc=$?; echo "hostenv $e rc=$rc: $(python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(d['value'], d['host_end_to_end'])" "$out/hostenv_$e.json")"
+            [ $rc -ne 0 ] && exit $rc
+        done ;;
     hosttrace)  # kernel + memory-copy trace of the host-buffer API (timeline of the pipeline)
         timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$out/hosttrace" -o run \
             --output-format csv -- python3 tools/host_e2e.py 268435456 T > "$out/hosttrace.log" 2>&1

@@ -1111,6 +1111,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             continue;
         }
         // ---------------- W-probe round (steps > 1)
+#ifdef SNAPPY_K1R_STATS
+        if constexpr (!BIG) n_farc++;  // (32 KiB units have no far gathers: the slot counts W-probe rounds)
+#endif
         lsw = false;
         if (p - 1 < q0 || p + 12 > q0 + 64) WINDOW_AT(p - 1);
         // lane k = k-th probe if all earlier miss, at its closed-form position
@@ -2010,6 +2013,12 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     uint32_t n_el = 0, n_batch = 0, n_pass = 0, n_sub = 0, n_far = 0;
     uint64_t sg0 = 0, sg1 = 0, sg2 = 0, ta, tb, tc, td;
 #endif
+#ifndef SNAPPY_K4_SPAN_ADAPT
+#define SNAPPY_K4_SPAN_ADAPT 1
+#endif
+    // the last batch was cut by the 1,024-byte output span (long copies): parse one
+    // half only -- more elements would be cut again (repeat-like data)
+    bool span_cut = false;
     while (st == SNAPPY_ST_OK && op < want) {
         if (ip >= clen) { st = SNAPPY_ST_TRUNCATED; break; }
         K4STAMP(ta);
@@ -2101,7 +2110,7 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             uint32_t hpos = o + xa;
 #pragma unroll
             for (int hh = 1; hh < SNAPPY_K4_HALVES; hh++) {
-                if (!(E < 64 && hpos <= 440)) break;
+                if (!(E < 64 && hpos <= 440) || (SNAPPY_K4_SPAN_ADAPT && span_cut)) break;
                 uint32_t bx0, bb4, eb, xb;
                 parse_half(hpos, bx0, bb4, eb, xb);
                 const int sa = (int)(4 * (lane - E));
@@ -2230,6 +2239,7 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             static_assert(2048 + kK4MapBits <= kK4Ring - 64, "K4: the ring must hold [F, op_end)");
             const uint64_t over = __ballot(lane < nexec && lane > 0 && out_off + e_len > kK4MapBits);
             if (over) nexec = (uint32_t)__builtin_ctzll(over);
+            span_cut = over != 0;
             if constexpr (BACK) {
                 // copies reading earlier units: wait until those bytes are in HBM
                 uint64_t bm = __ballot(e_back && lane < nexec);

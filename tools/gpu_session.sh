@@ -113,10 +113,27 @@ for step in "$@"; do
             python3 bench.py --steps 1 --warmup 1 --no-sub --no-cpu-baseline > "$out/hostinbench_trace.log" 2>&1
         rc=$?; echo "hostinbench trace rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
     hostenv)  # host_end_to_end inside a 1 GiB bench run: as is, with high-priority lane streams, with 8 hardware queues
-        for e in "X=1" "SNAPPY_AMD_PIPE_PRIO=1" "GPU_MAX_HW_QUEUES=8"; do
+        for e in ${HOSTENV_SET:-"X=1" "SNAPPY_AMD_PIPE_PRIO=1" "GPU_MAX_HW_QUEUES=8"}; do
             env $e timeout -k 10 300 python -u bench.py --total-bytes 1073741824 --steps 2 --warmup 1 --no-sub --no-cpu-baseline \
                 > "$out/hostenv_$e.json" 2> "$out/hostenv_$e.err"
             rc=$?; echo "hostenv $e rc=$rc: $(python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(d['value'], d['host_end_to_end'])" "$out/hostenv_$e.json")"
+            [ $rc -ne 0 ] && exit $rc
+        done ;;
+    hostctxab)  # host context's own stream at default vs high priority: tools/host_e2e.py twice each, then a trace of the latter
+        for r in 1 2; do for e in X=1 SNAPPY_AMD_HOSTCTX_PRIO=1; do
+            env $e timeout -k 10 120 python -u tools/host_e2e.py 268435456 T > "$out/hostctxab_${e}_$r.log" 2>&1
+            rc=$?; echo "hostctxab $e rc=$rc: $(grep -h '^T' "$out/hostctxab_${e}_$r.log")"; [ $rc -ne 0 ] && exit $rc
+        done; done
+        SNAPPY_AMD_HOSTCTX_PRIO=1 timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace -d "$out/hostctx_trace" -o run \
+            --output-format csv -- python3 tools/host_e2e.py 268435456 T > "$out/hostctx_trace.log" 2>&1
+        rc=$?; echo "hostctx trace rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
+    benchv:*)  # benchv:<variant,...>:<workload> -> bench.py --workload W per library variant (no sub-results, CPU or host legs)
+        IFS=: read -r _ vs wl <<< "$step"
+        for v in ${vs//,/ }; do
+            lib=""; [ "$v" != default ] && lib=$PWD/lightweight-snappy_amd/variants/libsnappy_amd_$v.so
+            SNAPPY_AMD_LIB=$lib timeout -k 10 300 python -u bench.py --workload $wl --steps 5 --warmup 2 --no-sub \
+                --no-cpu-baseline --no-host-e2e > "$out/benchv_${v}_$wl.json" 2> "$out/benchv_${v}_$wl.err"
+            rc=$?; echo "benchv $v $wl rc=$rc: $(python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(d['value'], d['kernel_ms'])" "$out/benchv_${v}_$wl.json")"
             [ $rc -ne 0 ] && exit $rc
         done ;;
     hosttrace)  # kernel + memory-copy trace of the host-buffer API (timeline of the pipeline)

@@ -39,3 +39,5 @@ print(f"{kind}: units {units} probes/unit {probes.mean():.0f} rounds/unit {round
 print(f"loop cycles/unit {loop.mean():.0f} cycles/probe {loop.sum() / probes.sum():.1f} cycles/round {loop.sum()/rounds.sum():.1f}"
       f" match-path cycles/match {tmatch.sum()/max(matches.sum(),1):.1f} non-match cycles/round {(loop.sum()-tmatch.sum())/rounds.sum():.1f}")
 print(f"64 KiB blocks: candidate gathers from global memory/unit {farc.mean():.1f}, ring segments loaded synchronously/unit {reload.mean():.1f}")
+if chunk <= 32768:
+    print(f"W-probe rounds (steps > 1) per unit {farc.mean():.0f} of {rounds.mean():.0f} rounds")

@@ -732,7 +732,23 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #define K1R_ASM_ROUNDS 0
 #endif
 #if K1R_ASM_ROUNDS
-#define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32)                                                  \
+// the candidate's register pair: 32 KiB units read registers c / 256, c / 256 + 1;
+// 65,536-byte blocks read ring registers (c / 256) mod 128 and the next, and leave
+// the loop for the C++ round (code 3) when the candidate's segment has left the
+// ring (a gather from global memory) or is the wrap pair 127 / 0
+#ifndef SNAPPY_K1R_ASM_BIG
+#define SNAPPY_K1R_ASM_BIG 1
+#endif
+#define K1R_CAND32 "s_lshr_b32 %[s0], %[c], 8\n\t"
+#define K1R_CAND64                                                                                  \
+    "s_lshr_b32 %[s0], %[c], 8\n\t"                                                                \
+    "s_add_u32 %[s1], %[s0], 128\n\t"                                                              \
+    "s_cmp_lt_u32 %[s1], %[seghi]\n\t"                                                             \
+    "s_cbranch_scc1 L%=_x3\n\t"                                                                    \
+    "s_and_b32 %[s0], %[s0], 127\n\t"                                                              \
+    "s_cmp_eq_u32 %[s0], 127\n\t"                                                                  \
+    "s_cbranch_scc1 L%=_x3\n\t"
+#define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, CAND, SEGHI)                                          \
     do {                                                                                            \
         uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4;                           \
         uint64_t _valid, _hm;                                                                       \
@@ -762,7 +778,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "v_add_u32_e32 %[t2], %[s0], %[lane4]\n\t"                                              \
             "ds_bpermute_b32 %[t2], %[t2], %[dv]\n\t" /* pa: dwords at pf */                        \
             "s_and_b32 %[c], %[c], 0xffff\n\t"                                                      \
-            "s_lshr_b32 %[s0], %[c], 8\n\t"                                                         \
+            CAND                                                                                    \
             "s_set_gpr_idx_on %[s0], gpr_idx(SRC0)\n\t"                                             \
             "v_mov_b32_e32 %[t3], v2\n\t"                                                           \
             "v_mov_b32_e32 %[t4], v3\n\t"                                                           \
@@ -878,7 +894,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
               [s3] "=&s"(_s3), [valid] "=&s"(_valid), [hm] "=&s"(_hm), [ent] "+v"(e32),              \
               [entt] "+v"(et32), [tka] "+v"(tka), [tkb] "+v"(tkb), [t0] "=&v"(_t0), [t1] "=&v"(_t1),  \
               [t2] "=&v"(_t2), [t3] "=&v"(_t3), [t4] "=&v"(_t4)                                       \
-            : [q0] "s"(q0), [L] "s"(L), [lm16] "s"(L - 16), [mwin] "s"(m_win), [dv] "v"(dv),         \
+            : [q0] "s"(q0), [L] "s"(L), [lm16] "s"(L - 16), [mwin] "s"(m_win), [seghi] SEGHI,         \
+              [dv] "v"(dv),                                                                         \
               [pdl1] "v"(pdl1), [pdc] "v"(pdc), [pdnz] "v"(pdnz), [adr] "v"(adr), [adrt] "v"(adr >> 1), \
               [word] "v"(word), [lane] "v"(lane), [lane4] "v"(lane << 2), [dummy] "v"(kDummy),         \
               [skipmax] "i"(64 - DMAX), [dmask] "i"((1u << DMAX) - 1), [lsmax] "i"(64 - SNAPPY_K1R_LSMIN), \
@@ -938,11 +955,14 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             TBL_READ_ENT(adr);
             for (;;) {
 #if K1R_ASM_ROUNDS
-                if constexpr (!BIG) {
+                if constexpr (!BIG || SNAPPY_K1R_ASM_BIG) {
                     // the common rounds as one hand-scheduled loop (k1r_asm_rounds below)
                     uint32_t code, fx, cx;
                     uint32_t e32 = ent, et32 = ent_t;
-                    K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32);
+                    if constexpr (BIG)
+                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND64, "s"(seg_hi));
+                    else
+                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND32, "i"(0));
                     ent = (uint16_t)e32;
                     ent_t = (uint8_t)et32;
                     if (code == 1) break;  // skip past the step-1 range, or is_block_end

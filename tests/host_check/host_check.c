@@ -161,22 +161,28 @@ static void round_trip_file(size_t n, int kind, uint64_t seed, int indexed)
     uint8_t *o = read_all(fo, &ol);
     CHECK(st == 0 && ol == n && memcmp(o, a, n) == 0, "FILE* decompress n=%zu indexed=%d: st %d got %zu", n, indexed,
           st, ol);
-    if (indexed && n > 65536) {  // an index entry that does not describe the stream is refused
+    if (indexed && n > 65536) {
         size_t xl;
         uint8_t *x = read_all(fx, &xl);
         CHECK(xl >= 40, "index length %zu", xl);
-        uint64_t e;
-        memcpy(&e, x + 32, 8);  // entry 1 (after magic, N, count, entry 0)
-        e += 1;
-        memcpy(x + 32, &e, 8);
-        FILE *fb = tmpfile(), *fo2 = tmpfile();
-        fwrite(x, 1, xl, fb);
-        rewind(fb);
-        rewind(fc);
-        st = snappy_decompress_file_indexed(fc, fb, fo2);
-        CHECK(st == SNAPPY_AMD_ERR_INDEX, "corrupted index: st %d", st);
-        fclose(fb);
-        fclose(fo2);
+        uint64_t e, e0;
+        memcpy(&e0, x + 32, 8);  // entry 1 (after magic, N, count, entry 0)
+        for (int k = 0; k < 2; k++) {
+            // k 0: entry 1 one byte off an element start -- the index still looks
+            // well-formed, so the decode reports the bad block (any error, no crash);
+            // k 1: entry 1 past the stream's end -- refused before any decoding
+            e = k == 0 ? e0 + 1 : (uint64_t)cl + 100;
+            memcpy(x + 32, &e, 8);
+            FILE *fb = tmpfile(), *fo2 = tmpfile();
+            fwrite(x, 1, xl, fb);
+            rewind(fb);
+            rewind(fc);
+            st = snappy_decompress_file_indexed(fc, fb, fo2);
+            if (k == 0) CHECK(st < 0, "index entry off by one byte: st %d", st);
+            else CHECK(st == SNAPPY_AMD_ERR_INDEX, "index entry past the stream: st %d", st);
+            fclose(fb);
+            fclose(fo2);
+        }
         free(x);
     }
     fclose(fi);

@@ -1104,3 +1104,20 @@ def test_host_buffer_pipelined_chunks():
         assert len(got) == len(want) and got == want, (kind, n)
         assert snappy_amd.decompress(got) == a.tobytes(), (kind, n)
         progress(f"pipelined host compress {kind} {n}: ok")
+
+
+def test_host_decompress_large_foreign():
+    """snappy_decompress_buffer of foreign streams of 34 and 115 MB (literals
+    of up to 200,000 bytes across K5p chunks and 65,536-byte blocks, copies up
+    to 1 MiB back) decodes as the oracle decodes them, and so does a stream of
+    ours just over 32 MiB."""
+    for seed, n_out in ((311, 112 << 20), (312, (33 << 20) + 200000)):
+        stream = build_stream(random_ops(seed, n_out, 1 << 20, max_lit=200000))
+        want = oracle.decompress(stream)
+        assert len(want) == n_out
+        assert snappy_amd.decompress(stream) == want, (seed, len(stream))
+        progress(f"host decompress of a foreign stream, seed {seed}: {len(stream)} stream bytes ok")
+    a = datagen.make("R", (32 << 20) + 4096, 313)
+    comp = snappy_amd.compress(a.tobytes())
+    assert len(comp) > (32 << 20)
+    assert snappy_amd.decompress(comp) == a.tobytes()

@@ -119,6 +119,17 @@ for step in "$@"; do
             rc=$?; echo "hostenv $e rc=$rc: $(python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(d['value'], d['host_end_to_end'])" "$out/hostenv_$e.json")"
             [ $rc -ne 0 ] && exit $rc
         done ;;
+    hostenvab:*)  # hostenvab:<ENV=V+ENV=V,...> -> tools/host_e2e.py (text 256 MiB) per env set, twice, interleaved
+        sets=${step#hostenvab:}
+        for r in 1 2; do for e in ${sets//,/ }; do
+            env ${e//+/ } timeout -k 10 120 python -u tools/host_e2e.py 268435456 T > "$out/hostenvab_${e}_$r.log" 2>&1
+            rc=$?; echo "hostenvab $e rc=$rc: $(grep -h '^T' "$out/hostenvab_${e}_$r.log")"; [ $rc -ne 0 ] && exit $rc
+        done; done ;;
+    hosttraceenv:*)  # hosttraceenv:<ENV=V+...> -> kernel + memory-copy trace of tools/host_e2e.py under that env
+        e=${step#hosttraceenv:}
+        env ${e//+/ } timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace -d "$out/hosttraceenv" -o run \
+            --output-format csv -- python3 tools/host_e2e.py 268435456 T > "$out/hosttraceenv.log" 2>&1
+        rc=$?; echo "hosttraceenv rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
     hostctxab)  # host context's own stream at default vs high priority: tools/host_e2e.py twice each, then a trace of the latter
         for r in 1 2; do for e in X=1 SNAPPY_AMD_HOSTCTX_PRIO=1; do
             env $e timeout -k 10 120 python -u tools/host_e2e.py 268435456 T > "$out/hostctxab_${e}_$r.log" 2>&1

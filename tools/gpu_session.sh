@@ -130,6 +130,13 @@ for step in "$@"; do
         env ${e//+/ } timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace -d "$out/hosttraceenv" -o run \
             --output-format csv -- python3 tools/host_e2e.py 268435456 T > "$out/hosttraceenv.log" 2>&1
         rc=$?; echo "hosttraceenv rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
+    fileab:*)  # fileab:<ENV=V+...,...> -> bench.host_file_api (4 GiB text in /dev/shm, IO trace) per env set, twice, interleaved
+        sets=${step#fileab:}
+        for r in 1 2; do for e in ${sets//,/ }; do
+            env SNAPPY_AMD_IO_TRACE=1 ${e//+/ } timeout -k 10 200 python -u -c "import json, bench; print(json.dumps(bench.host_file_api(4 << 30)))" \
+                > "$out/fileab_${e}_$r.log" 2>&1
+            rc=$?; echo "fileab $e rc=$rc: $(grep -h 'compress_MBps' "$out/fileab_${e}_$r.log")"; [ $rc -ne 0 ] && exit $rc
+        done; done ;;
     hostctxab)  # host context's own stream at default vs high priority: tools/host_e2e.py twice each, then a trace of the latter
         for r in 1 2; do for e in X=1 SNAPPY_AMD_HOSTCTX_PRIO=1; do
             env $e timeout -k 10 120 python -u tools/host_e2e.py 268435456 T > "$out/hostctxab_${e}_$r.log" 2>&1

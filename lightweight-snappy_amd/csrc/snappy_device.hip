@@ -612,6 +612,44 @@ void par_copy(uint8_t *dst, const uint8_t *src, size_t len)
 // extended to the bound while mapped and cut back to max(its old size, the
 // bytes written) by finish() (or by the destructor on an error path);
 // SNAPPY_AMD_NO_MMAP=1 keeps pwrite().
+// Unmapping a large populated output mapping tears down its page tables
+// (≈ 0.2 s for 4 GiB on the GPU box), after the file's bytes and size are
+// final: a successful mapped writer hands the munmap (and the close of its
+// read-write descriptor) to a background thread instead of waiting for it.
+// Pending unmaps are joined by the next one queued and at exit.
+// SNAPPY_AMD_SYNC_UNMAP=1 unmaps in the call.
+struct UnmapReaper {
+    std::mutex mu;
+    std::vector<std::thread> ts;
+    void queue(void *map, size_t len, int close_fd)
+    {
+        std::vector<std::thread> done;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            done.swap(ts);
+            ts.emplace_back([map, len, close_fd] {
+                (void)munmap(map, len);
+                if (close_fd >= 0) ::close(close_fd);
+            });
+        }
+        for (auto &t : done) t.join();
+    }
+    ~UnmapReaper()
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (auto &t : ts) t.join();
+    }
+};
+UnmapReaper g_reaper;
+bool async_unmap()
+{
+    static const bool a = [] {
+        const char *e = getenv("SNAPPY_AMD_SYNC_UNMAP");
+        return !(e && atoi(e) != 0);
+    }();
+    return a;
+}
+
 struct IoFile {
     FILE *f = nullptr;
     int fd = -1;
@@ -682,13 +720,18 @@ struct IoFile {
     }
     // unmap; the file keeps max(its old size, the end of the bytes written) --
     // its old size if nothing was written (an error before the first chunk)
-    bool unmap()
+    bool unmap(bool background = false)
     {
         if (!map) return true;
-        bool ok = munmap(map, map_len) == 0;
         const uint64_t keep = pos > map_from ? std::max(old_size, pos) : old_size;
-        if (map_end > keep) ok = ftruncate(map_fd, (off_t)keep) == 0 && ok;
-        if (map_fd != fd) ::close(map_fd);
+        bool ok = true;
+        if (background && map_end <= keep && async_unmap()) {  // nothing to cut back: bytes and size are final
+            g_reaper.queue(map, map_len, map_fd != fd ? map_fd : -1);
+        } else {
+            ok = munmap(map, map_len) == 0;
+            if (map_end > keep) ok = ftruncate(map_fd, (off_t)keep) == 0 && ok;
+            if (map_fd != fd) ::close(map_fd);
+        }
         map = nullptr;
         map_fd = -1;
         return ok;
@@ -715,7 +758,7 @@ struct IoFile {
         return put == len;
     }
     bool error() const { return !pos_io && ferror(f); }
-    bool finish() { return unmap() && (!pos_io || fseeko(f, (off_t)pos, SEEK_SET) == 0); }
+    bool finish() { return unmap(true) && (!pos_io || fseeko(f, (off_t)pos, SEEK_SET) == 0); }
 };
 
 void slot_free(StreamSlot &s)
@@ -1322,14 +1365,15 @@ int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count
     wr.wait();
     t_wr = wr.busy;
     if (!wr.ok) return SNAPPY_AMD_ERR_IO;
+    const double t4 = io_now();
     const bool fin_ok = out.finish();
     pre.ok = fin_ok;
     if (io_trace())
         fprintf(stderr, "[snappy_amd io] decompress %llu -> %llu B: in %.3f s (reads %.3f), index+decode %.3f s, "
-                        "preallocation wait %.3f s, out %.3f s (copy waits %.3f, writer waits %.3f, writes %.3f), "
-                        "%d/%d threads, positional out %d mapped %d\n",
+                        "preallocation wait %.3f s, out %.3f s (copy waits %.3f, writer waits %.3f, writes %.3f, "
+                        "finish %.3f), %d/%d threads, positional out %d mapped %d\n",
                 (unsigned long long)n, (unsigned long long)N, t1 - t0, t_rd, t2 - t1, t3 - t2, io_now() - t3, t_ev,
-                t_join, t_wr,
+                t_join, t_wr, io_now() - t4,
                 io_threads(), io_wthreads(), (int)out.pos_io, (int)out_mapped);
     return fin_ok ? SNAPPY_AMD_OK : SNAPPY_AMD_ERR_IO;
 }

@@ -1121,3 +1121,28 @@ def test_host_decompress_large_foreign():
     comp = snappy_amd.compress(a.tobytes())
     assert len(comp) > (32 << 20)
     assert snappy_amd.decompress(comp) == a.tobytes()
+
+
+def test_file_decompress_back_to_back_outputs():
+    """The FILE* decoder's mapped output is unmapped in the background once
+    its bytes and size are final (IoFile::unmap): the output reads back whole
+    right after the call, and the same path can be removed, rewritten and
+    decoded into again at once, three times in a row."""
+    import ctypes
+    libc = ctypes.CDLL(None)
+    libc.fopen.restype = ctypes.c_void_p
+    libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    libc.fclose.argtypes = [ctypes.c_void_p]
+    lib = snappy_amd.lib()
+    data = datagen.make("T", (96 << 20) + 777, 91).tobytes()
+    comp = snappy_amd.compress(data)
+    with tempfile.TemporaryDirectory(dir="/dev/shm" if os.path.isdir("/dev/shm") else None) as d:
+        src, dst = os.path.join(d, "in.snp"), os.path.join(d, "out")
+        open(src, "wb").write(comp)
+        for _ in range(3):
+            fi, fo = libc.fopen(src.encode(), b"rb"), libc.fopen(dst.encode(), b"wb")
+            assert lib.snappy_decompress(ctypes.c_void_p(fi), ctypes.c_void_p(fo)) == 0
+            libc.fclose(fi), libc.fclose(fo)
+            assert os.path.getsize(dst) == len(data)
+            assert open(dst, "rb").read() == data
+            os.unlink(dst)

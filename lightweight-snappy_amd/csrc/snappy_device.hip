@@ -11,6 +11,8 @@
 #include <fcntl.h>
 #include <memory>
 #include <mutex>
+#include <new>
+#include <pthread.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <thread>
@@ -619,28 +621,51 @@ void par_copy(uint8_t *dst, const uint8_t *src, size_t len)
 // Pending unmaps are joined by the next one queued and at exit.
 // SNAPPY_AMD_SYNC_UNMAP=1 unmaps in the call.
 struct UnmapReaper {
+    struct Job {
+        void *map;
+        size_t len;
+        int close_fd;
+    };
     std::mutex mu;
-    std::vector<std::thread> ts;
+    std::vector<pthread_t> ts;  // (raw ids: a forked child forgets its parent's, see below)
+    static void *run(void *a)
+    {
+        const Job *j = static_cast<Job *>(a);
+        (void)munmap(j->map, j->len);
+        if (j->close_fd >= 0) ::close(j->close_fd);
+        delete j;
+        return nullptr;
+    }
+    UnmapReaper()
+    {
+        // a child forked while an unmap runs has no such thread: it must not join it at exit
+        (void)pthread_atfork(nullptr, nullptr, [] { g_reaper_forget(); });
+    }
+    static void g_reaper_forget();
     void queue(void *map, size_t len, int close_fd)
     {
-        std::vector<std::thread> done;
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            done.swap(ts);
-            ts.emplace_back([map, len, close_fd] {
-                (void)munmap(map, len);
-                if (close_fd >= 0) ::close(close_fd);
-            });
-        }
-        for (auto &t : done) t.join();
+        Job *j = new Job{map, len, close_fd};
+        std::vector<pthread_t> done;
+        pthread_t t;
+        std::lock_guard<std::mutex> lk(mu);
+        done.swap(ts);
+        if (pthread_create(&t, nullptr, run, j) == 0) ts.push_back(t);
+        else run(j);  // no thread: unmap here
+        for (pthread_t d : done) pthread_join(d, nullptr);
     }
     ~UnmapReaper()
     {
         std::lock_guard<std::mutex> lk(mu);
-        for (auto &t : ts) t.join();
+        for (pthread_t t : ts) pthread_join(t, nullptr);
+        ts.clear();
     }
 };
 UnmapReaper g_reaper;
+void UnmapReaper::g_reaper_forget()  // (the child is single-threaded: a lock held at fork is reset)
+{
+    new (&g_reaper.mu) std::mutex();
+    g_reaper.ts.clear();
+}
 bool async_unmap()
 {
     static const bool a = [] {

@@ -2793,13 +2793,14 @@ __device__ __forceinline__ void k5_chain(const uint8_t *__restrict__ comp, uint3
         const bool e_ok = (s_hi >> 31) == 0;
         const uint64_t e_size = ((uint64_t)(s_hi & 0x7FFFFFFFu) << 32) | s_lo;
         const uint64_t e_len = ((uint64_t)l_hi << 32) | l_lo;
-        // exclusive prefix sums (64-bit values < 2^33, as 16-bit low parts + the rest)
-        uint32_t t0, t1, t2, t3;
-        const uint32_t sl = wave_excl_scan32(live ? (uint32_t)e_size & 0xFFFF : 0u, &t0);
-        const uint32_t sh = wave_excl_scan32(live ? (uint32_t)(e_size >> 16) : 0u, &t1);
+        // element k's relative start is x + pos: the exclusive sum of the live
+        // sizes before it, every one of which ended inside the window (< 64);
+        // output offsets: exclusive prefix sums of the lengths (64-bit values
+        // < 2^33, as 16-bit low parts + the rest)
+        uint32_t t2, t3;
         const uint32_t ll = wave_excl_scan32(live ? (uint32_t)e_len & 0xFFFF : 0u, &t2);
         const uint32_t lh = wave_excl_scan32(live ? (uint32_t)(e_len >> 16) : 0u, &t3);
-        const uint64_t e_x = x + ((uint64_t)sh << 16) + sl;  // relative start
+        const uint64_t e_x = x + pos;  // relative start
         const uint64_t e_op = op + ((uint64_t)lh << 16) + ll;
         // the first element that ends the walk: a bad header (both), a truncated
         // element (MARK), or (MARK) one at or past N (not run) / past N (run, then OVERRUN)

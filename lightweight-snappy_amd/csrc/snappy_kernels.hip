@@ -2980,6 +2980,29 @@ __global__ __launch_bounds__(64) void k5b_carry(const uint8_t *__restrict__ comp
     const uint64_t N = h.N;
     uint64_t E = h.len, base = 0;
     uint64_t xa[K5_G], oa[K5_G], xb[K5_G], ob_[K5_G];
+    // walk lookahead: a run of long elements (incompressible data: one literal
+    // per block, so a walk per block, each step a dependent global load) is
+    // parsed 64 elements per load round trip -- after a miss parses the element
+    // at x, lane k parses the one at x + k * size (the next ones, if they repeat
+    // its size); later walks look their start up first.  A parse depends only on
+    // its position, so a hit equals the load it replaces.
+    uint64_t la_x = ~0ull, la_size = 0, la_len = 0;
+    bool la_ok = false;
+    auto parse_la = [&](uint64_t x, uint64_t &size, uint64_t &len) -> bool {
+        const uint64_t m = __ballot(la_x == x);
+        if (m) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(m);
+            size = rl64(la_size, k);
+            len = rl64(la_len, k);
+            return __builtin_amdgcn_readlane((uint32_t)la_ok, k) != 0;
+        }
+        const bool ok = k5_parse(comp, clen, x, size, len);
+        if (ok && size >= 64) {
+            la_x = x + (uint64_t)lane * size;
+            la_ok = k5_parse(comp, clen, la_x, la_size, la_len);
+        }
+        return ok;
+    };
     auto load = [&](uint32_t g, uint64_t *xs, uint64_t *os) {
 #pragma unroll
         for (uint32_t j = 0; j < K5_G; j++) {
@@ -3011,7 +3034,7 @@ __global__ __launch_bounds__(64) void k5b_carry(const uint8_t *__restrict__ comp
                 uint64_t x = E;
                 while (x < end && base < N) {
                     uint64_t size, len;
-                    if (!k5_parse(comp, clen, x, size, len)) {
+                    if (!parse_la(x, size, len)) {
                         x = clen + 1;
                         break;
                     }

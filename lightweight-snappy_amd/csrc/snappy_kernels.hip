@@ -3011,43 +3011,60 @@ __global__ __launch_bounds__(64) void k5b_carry(const uint8_t *__restrict__ comp
             os[j] = c < nchunks ? O[c * 64 + lane] : 0;
         }
     };
+    uint32_t lookups = 0;  // K5a lookups in the current chunk-by-chunk block
+    // chunk c: its entry and base, then the chain through it (a K5a lookup by
+    // `look`, or a walk)
+    auto step = [&](uint32_t c, auto look) {
+        const uint64_t c0 = h.len + (uint64_t)c * K5_S;
+        const uint64_t end = c0 + K5_S < clen ? c0 + K5_S : clen;
+        if (h.st != SNAPPY_ST_OK || base >= N || E >= end) {
+            if (lane == 0) Ent[c] = K5_SKIP;
+            return;
+        }
+        if (lane == 0) {
+            Ent[c] = E;
+            Base[c] = base;
+        }
+        if (E - c0 < 64) {
+            uint64_t xo, oo;
+            look((uint32_t)(E - c0), xo, oo);
+            base += oo;
+            E = xo;
+            lookups++;
+        } else {  // entered past byte 63 (after a long literal): walk the chunk
+            uint64_t x = E;
+            while (x < end && base < N) {
+                uint64_t size, len;
+                if (!parse_la(x, size, len)) {
+                    x = clen + 1;
+                    break;
+                }
+                base += len;
+                x += size;
+            }
+            E = x;
+        }
+    };
     auto run = [&](uint32_t g, const uint64_t *xs, const uint64_t *os) {
 #pragma unroll
         for (uint32_t j = 0; j < K5_G; j++) {
             const uint32_t c = g * K5_G + j;
             if (c >= nchunks) break;
-            const uint64_t c0 = h.len + (uint64_t)c * K5_S;
-            const uint64_t end = c0 + K5_S < clen ? c0 + K5_S : clen;
-            if (h.st != SNAPPY_ST_OK || base >= N || E >= end) {
-                if (lane == 0) Ent[c] = K5_SKIP;
-                continue;
-            }
-            if (lane == 0) {
-                Ent[c] = E;
-                Base[c] = base;
-            }
-            if (E - c0 < 64) {
-                const uint32_t l = (uint32_t)(E - c0);
-                base += rl64(os[j], l);
-                E = rl64(xs[j], l);
-            } else {  // entered past byte 63 (after a long literal): walk the chunk
-                uint64_t x = E;
-                while (x < end && base < N) {
-                    uint64_t size, len;
-                    if (!parse_la(x, size, len)) {
-                        x = clen + 1;
-                        break;
-                    }
-                    base += len;
-                    x += size;
-                }
-                E = x;
-            }
+            step(c, [&](uint32_t l, uint64_t &xo, uint64_t &oo) {
+                xo = rl64(xs[j], l);
+                oo = rl64(os[j], l);
+            });
         }
     };
     static_assert(64 % K5_G == 0, "K5_G divides a 64-chunk block");
     constexpr uint32_t kGB = 64 / K5_G;  // prefetch groups per block
     const uint32_t nblk = (nchunks + 63) / 64;
+    // a chunk-by-chunk block whose predecessor of that kind needed fewer than
+    // kDemand lookups (runs of long literals: incompressible data) loads its
+    // lookups on demand and skips the chunks its chain jumps over, instead of
+    // prefetching every chunk's 64-entry rows (a load round trip per 8 chunks)
+    constexpr uint32_t kDemand = 8;
+    bool demand = false;
     uint64_t fr = F[lane];  // block 0's composed map, then each next one a block ahead
     for (uint32_t B = 0; B < nblk; B++) {
         const uint64_t fn = B + 1 < nblk ? F[64 * (uint64_t)(B + 1) + lane] : kK5Esc64;
@@ -3068,14 +3085,36 @@ __global__ __launch_bounds__(64) void k5b_carry(const uint8_t *__restrict__ comp
         }
         if (!fast) {
             if (lane == 0) BE[B] = K5_SKIP;
-            const uint32_t g0 = B * kGB;
-            load(g0, xa, oa);
-            for (uint32_t g = g0; g < g0 + kGB; g += 2) {
-                load(g + 1, xb, ob_);
-                run(g, xa, oa);
-                if (g + 2 < g0 + kGB) load(g + 2, xa, oa);
-                run(g + 1, xb, ob_);
+            lookups = 0;
+            const uint32_t cb = 64 * B, ce = cb + 64 < nchunks ? cb + 64 : nchunks;
+            if (demand) {
+                for (uint32_t c = cb; c < ce;) {
+                    // chunks the chain jumps over (entry past their end) are skipped at once
+                    const uint64_t cc0 = h.len + (uint64_t)c * K5_S;
+                    if (h.st == SNAPPY_ST_OK && base < N && E >= cc0 + K5_S && E < clen) {
+                        const uint64_t cj = (E - h.len) / K5_S;
+                        const uint32_t cn = cj < ce ? (uint32_t)cj : ce;
+                        if (c + lane < cn) Ent[c + lane] = K5_SKIP;  // (cn - c <= 64)
+                        c = cn;
+                        continue;
+                    }
+                    step(c, [&](uint32_t l, uint64_t &xo, uint64_t &oo) {
+                        xo = X[(uint64_t)c * 64 + l];
+                        oo = O[(uint64_t)c * 64 + l];
+                    });
+                    c++;
+                }
+            } else {
+                const uint32_t g0 = B * kGB;
+                load(g0, xa, oa);
+                for (uint32_t g = g0; g < g0 + kGB; g += 2) {
+                    load(g + 1, xb, ob_);
+                    run(g, xa, oa);
+                    if (g + 2 < g0 + kGB) load(g + 2, xa, oa);
+                    run(g + 1, xb, ob_);
+                }
             }
+            demand = lookups < kDemand;
         }
         fr = fn;
     }

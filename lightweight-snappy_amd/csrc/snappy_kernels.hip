@@ -275,7 +275,7 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
                            // 9 / 10 / 12: 16.07 / 16.19 / 16.18 ms per GiB, profiles/r03s2z_*, r03s2aa_*)
 #endif
 #ifndef SNAPPY_K1R_DMAX64
-#define SNAPPY_K1R_DMAX64 10  // K1r64 (65,536-byte blocks): 9 / 10 / 12 -> 19.29 / 19.23 / 19.32 ms
+#define SNAPPY_K1R_DMAX64 9  // K1r64 (65,536-byte blocks), with the asm round loop: 9 / 10 / 11 / 12 -> 18.70-18.73 / 18.81-18.82 / 18.75 / 18.81-18.84 ms
 #endif
 #ifndef SNAPPY_K1R_LSMIN
 #define SNAPPY_K1R_LSMIN 4  // lane-space rounds while at least this many step-1 probes remain

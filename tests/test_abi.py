@@ -136,7 +136,8 @@ def test_kernel_register_budget(tmp_path):
     if not (os.path.exists(obj) and os.path.exists(f"{llvm}/llvm-objdump") and shutil.which("objcopy")):
         pytest.skip("needs the in-tree build object and the ROCm LLVM tools")
     fat, co = tmp_path / "fat.bin", tmp_path / "k.co"
-    subprocess.run(["objcopy", f"--dump-section=.hip_fatbin={fat}", obj], check=True)
+    # (an output file: with none, objcopy rewrites the build object in place)
+    subprocess.run(["objcopy", f"--dump-section=.hip_fatbin={fat}", obj, str(tmp_path / "copy.o")], check=True)
     subprocess.run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
                     "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
     notes = subprocess.run([f"{llvm}/llvm-readobj", "--notes", str(co)], check=True, capture_output=True,
@@ -170,7 +171,7 @@ def test_asm_memory_ops_drained(tmp_path, obj):
     if not (os.path.exists(path) and os.path.exists(f"{llvm}/llvm-objdump") and shutil.which("objcopy")):
         pytest.skip("needs the in-tree build object and the ROCm LLVM tools")
     fat, co = tmp_path / "fat.bin", tmp_path / "k.co"
-    subprocess.run(["objcopy", f"--dump-section=.hip_fatbin={fat}", path], check=True)
+    subprocess.run(["objcopy", f"--dump-section=.hip_fatbin={fat}", path, str(tmp_path / "copy.o")], check=True)
     subprocess.run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
                     "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
     dis = subprocess.run([f"{llvm}/llvm-objdump", "-d", str(co)], check=True, capture_output=True, text=True).stdout

@@ -9,9 +9,8 @@ Workloads (BASELINE.json configs):
                    64 GiB of synthetic enwik8-like text as 2,097,152
                    independent 32 KiB streams (each == the reference's
                    snappy_compress() of its chunk), strong-scaled over the N
-                   ranks (rank r owns the unit-aligned range
-                   dist.shard_range(64 GiB, N, r)), so --gpus 1/2/4/8 is one
-                   job on one curve.  At N = 1 the same JSON line carries
+                   ranks (1 GiB global pieces, block-cyclic), so --gpus
+                   1/2/4/8 is one job on one curve.  At N = 1 the same JSON line carries
                    compact sub-results for the other configs -- text32k
                    (configs[1]: 1 GiB of the same streams), text64k (one
                    snappy_compress() stream of 64 KiB blocks), random +
@@ -24,13 +23,17 @@ Workloads (BASELINE.json configs):
   --weak / --bytes-per-gpu B   B bytes per rank (default 1 GiB).
   --total-bytes T  any fixed job size, strong-scaled.
 
-Exchange steps: C1, the all-gather of the shard sizes, is part
-of every step.  With N > 1 a second timed loop runs the whole job end to
-end -- compress, C1, C2 (RCCL all-gather of the compressed shards, padded:
-RCCL has no all-gatherv), compaction into the contiguous stream every rank
-then holds, decompress of the rank's blocks from that stream -- and reports
-it as `value_end_to_end`.  C3 (all-gather of the decoded shards) is opt-in
-(--c3).  Every phase is checked (round trip, per-shard checksums).
+Sharding is block-cyclic (dist.piece_plan): the job is cut into global pieces
+(--e2e-piece-bytes, default a quarter of a share, <= 1 GiB) and piece g belongs
+to rank g mod N.  Exchange steps: C1, the all-gather of the
+shard sizes, is part of every step of the timed loop (`value`: the per-rank
+compute curve).  With N > 1 a second timed loop runs the whole job end to end
+as a pipeline -- per step: compress the rank's piece, C1, C2 (RCCL all-gather
+of the step's payloads, padded: RCCL has no all-gatherv) copied into the
+contiguous stream every rank then holds, decode of the rank's piece from that
+stream; C2 and the decode overlap the next step's compress -- and reports it
+as `value_end_to_end`.  C3 (all-gather of the decoded shards) is opt-in
+(--c3).  Every phase is checked (round trip, per-piece checksums).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
                        [--workload text32k|text64k|random|repeat|decode10g]
@@ -61,7 +64,8 @@ import torch.distributed as dist  # noqa: E402
 
 import datagen  # noqa: E402
 import snappy_amd  # noqa: E402
-from dist import HBM_BYTES, pieces_of, rank_plan, shard_range  # noqa: E402
+from dist import (C2_MAX_BYTES, HBM_BYTES, c2_gather_step, default_e2e_piece, piece_plan, piece_step, pieces_of,  # noqa: E402
+                  pipeline_steps, rank_plan)
 
 METRIC = "compress + decompress MB/s at 1/2/4/8 MI355X; % HBM roofline; ratio vs ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -101,6 +105,16 @@ def parse(argv=None):
     ap.add_argument("--piece-bytes", type=int, default=8 * GiB,
                     help="a rank compresses its range in pieces of at most this many bytes (bounds token scratch)")
     ap.add_argument("--no-assemble", action="store_true", help="N > 1: skip the end-to-end loop with C2")
+    ap.add_argument("--e2e-piece-bytes", type=int, default=0,
+                    help="the job's global piece (block-cyclic sharding, one pipeline step of the end-to-end loop "
+                         "per piece per rank; default dist.default_e2e_piece: a quarter of a share, <= 1 GiB)")
+    ap.add_argument("--c2-max-bytes", type=int, default=C2_MAX_BYTES,
+                    help="one C2 all-gather sends at most this many bytes per rank (a step's larger payload is "
+                         "gathered in several)")
+    ap.add_argument("--e2e-dump", default=None,
+                    help="rank 0 writes the reassembled stream of the end-to-end loop to this file (tests)")
+    ap.add_argument("--no-e2e-overlap", action="store_true",
+                    help="end-to-end loop: run each step's C2 and decode before the next step's compress (A/B)")
     ap.add_argument("--c3", action="store_true", help="N > 1: also time C3, the all-gather of the decoded shards")
     ap.add_argument("--e2e-steps", type=int, default=3, help="N > 1: steps of the end-to-end loop")
     ap.add_argument("--overlap", action="store_true",
@@ -438,9 +452,9 @@ def load_pmc(path, workload: str, n: int) -> dict:
 
 
 class Piece:
-    """A unit-aligned part of the rank's range, compressed into its own slice
-    of the rank's contiguous payload (pieces after the stream's first carry no
-    varint preamble in the SINGLE layout)."""
+    """A unit-aligned launch over part of the rank's input x, compressed into
+    its own slice of the rank's payload (only the stream's first launch
+    carries the SINGLE varint preamble)."""
 
     def __init__(self, off: int, n: int, flags: int):
         self.off, self.n, self.flags = off, n, flags
@@ -449,39 +463,64 @@ class Piece:
         self.offs = None
 
 
-class Job:
-    """One workload's buffers on this rank: the input range in HBM, the payload
-    (sized for the job's largest shard, equal on every rank), the decoded
-    output and the per-piece block indexes."""
+class GPiece:
+    """One of the rank's global pieces (dist.piece_plan): global piece g at
+    global offset goff, held at x[xoff:xoff+n]; in the end-to-end loop it is
+    compressed into payload slot k (out[k*slot:]) and gathered in step k."""
 
-    def __init__(self, name, codec, dev, n, r_off, total_in, n_max, piece_bytes, keep_size=False):
+    def __init__(self, k: int, g: int, goff: int, xoff: int, n: int, flags: int):
+        self.k, self.g, self.goff, self.xoff, self.n, self.flags = k, g, goff, xoff, n, flags
+        self.clen = 0
+        self.offs = None
+
+
+class Job:
+    """One workload's buffers on this rank: the input (the rank's global
+    pieces back to back) in HBM, the payload, the decoded output and the
+    per-launch block indexes.  The timed loop compresses x in launches of
+    <= piece_bytes (the compressed pieces packed); the end-to-end loop per
+    global piece into fixed slots (dist.rank_plan sizes `out` for both)."""
+
+    def __init__(self, name, codec, dev, gpieces, total_in, piece_bytes, e2e_piece, steps_e2e, keep_size=False):
         kind, seed, layout, chunk, desc = WORKLOADS[name]
         self.name, self.kind, self.seed, self.layout, self.chunk, self.desc = name, kind, seed, layout, chunk, desc
         self.codec, self.dev = codec, dev
         self.decode_only = name in DECODE_ONLY
         self.unit = chunk if layout == snappy_amd.STREAMS else 65536
-        self.n, self.r_off, self.total_in = n, r_off, total_in
-        # the rank's range in HBM, generated on the host 1 GiB at a time
+        n = sum(m for _, _, m in gpieces)
+        self.n, self.total_in = n, total_in
+        self.gpieces = []
+        xo = 0
+        for k, (g, goff, m) in enumerate(gpieces):
+            flags = snappy_amd.NO_PREAMBLE if (layout == snappy_amd.SINGLE and goff > 0) else 0
+            self.gpieces.append(GPiece(k, g, goff, xo, m, flags))
+            xo += m
+        # the rank's pieces in HBM, generated on the host 1 GiB at a time
         self.x = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
         host = np.empty(min(max(n, 1), GiB), dtype=np.uint8)
-        for o in range(0, n, GiB):
-            m = min(GiB, n - o)
-            datagen.fill(host[:m], kind, seed, offset=r_off + o, threads=16)
-            self.x[o:o + m].copy_(torch.from_numpy(host[:m]))
+        for gp in self.gpieces:
+            for o in range(0, gp.n, GiB):
+                m = min(GiB, gp.n - o)
+                datagen.fill(host[:m], kind, seed, offset=gp.goff + o, threads=16)
+                self.x[gp.xoff + o:gp.xoff + o + m].copy_(torch.from_numpy(host[:m]))
         del host
         self.units = codec.num_units(n, chunk, layout)
+        # the timed loop's launches over x: x[0] is global offset 0 only on the rank owning piece 0
+        first_global = bool(self.gpieces) and self.gpieces[0].goff == 0
         self.pieces = []
         o = 0
         for m in pieces_of(n, self.unit, piece_bytes):
-            flags = snappy_amd.NO_PREAMBLE if (layout == snappy_amd.SINGLE and (r_off + o) > 0) else 0
+            flags = snappy_amd.NO_PREAMBLE if (layout == snappy_amd.SINGLE and (o > 0 or not first_global)) else 0
             self.pieces.append(Piece(o, m, flags))
             o += m
-        cap = sum(codec.max_output(m, chunk, layout) for m in pieces_of(n_max, self.unit, piece_bytes))
-        self.out_cap = max(cap, 16)
+        self.e2e_piece, self.steps_e2e = e2e_piece, steps_e2e
+        self.slot = codec.max_output(e2e_piece, chunk, layout)
+        cap = sum(codec.max_output(m, chunk, layout) for m in pieces_of(n, self.unit, piece_bytes))
+        self.out_cap = max(cap, steps_e2e * self.slot, 16)
         self.out = torch.empty(self.out_cap, dtype=torch.uint8, device=dev)
         for p in self.pieces:
             p.offs = torch.empty(codec.num_units(p.n, chunk, layout) + 1, dtype=torch.int64, device=dev)
-        self.back = torch.empty(max(n_max, 1), dtype=torch.uint8, device=dev)
+        self.back = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
         # SINGLE layout: the stream's first piece carries the global preamble
         self.header_value = total_in if layout == snappy_amd.SINGLE else n
         self.pre_clen = None
@@ -556,7 +595,7 @@ class Job:
     def free(self):
         for a in ("x", "out", "back", "g_offs"):
             setattr(self, a, None)
-        for p in self.pieces:
+        for p in self.pieces + self.gpieces:
             p.offs = None
         torch.cuda.empty_cache()
 
@@ -657,7 +696,7 @@ def sub_result(name: str, codec, dev, steps: int, warmup: int, piece_bytes: int,
     CPU baseline on a 64 MiB sample of the same workload."""
     n = DECODE10G_BYTES if name in DECODE_ONLY else GiB
     t_gen = time.perf_counter()
-    job = Job(name, codec, dev, n, 0, n, n, piece_bytes)
+    job = Job(name, codec, dev, [(0, 0, n)], n, piece_bytes, n, 1)
     t_gen = time.perf_counter() - t_gen
     elapsed, clen, k1, k3, k4 = timed_steps(job, steps, warmup, 1)
     ok = job.verify()
@@ -682,25 +721,29 @@ def sub_result(name: str, codec, dev, steps: int, warmup: int, piece_bytes: int,
 
 
 def resolve_sizes(args, world: int, rank: int):
-    """(strong, total input bytes, this rank's offset, its bytes, the largest
-    rank's bytes).  Without size flags: configs[3] (64 GiB in total, strong
-    scaling) for text32k at every N -- so --gpus 1/2/4/8 is one job on one
-    curve -- and for every other compressing workload at N > 1; another
-    workload alone at N = 1 is 1 GiB (decode10g: its ~10 GB stream)."""
+    """(strong, total input bytes, this rank's global pieces [(g, offset,
+    bytes)], its bytes, the end-to-end piece, the pipeline's steps).
+    Without size flags: configs[3] (64 GiB in total, strong scaling) for
+    text32k at every N -- so --gpus 1/2/4/8 is one job on one curve -- and
+    for every other compressing workload at N > 1; another workload alone at
+    N = 1 is 1 GiB (decode10g: its ~10 GB stream).  Sharding is block-cyclic
+    in pieces of --e2e-piece-bytes (dist.piece_plan; at N = 1 the whole
+    range)."""
     kind, seed, layout, chunk, desc = WORKLOADS[args.workload]
     unit = chunk if layout == snappy_amd.STREAMS else 65536
     total = args.total_bytes
     weak = args.weak or args.bytes_per_gpu is not None
     if total == 0 and not weak and args.workload not in DECODE_ONLY and (world > 1 or args.workload == "text32k"):
         total = CONFIG3_BYTES
-    if total > 0:
-        r_off, n = shard_range(total, world, rank, unit)
-        n_max = max(shard_range(total, world, r, unit)[1] for r in range(world))
-        return True, total, r_off, n, n_max
-    n = args.bytes_per_gpu if args.bytes_per_gpu is not None else GiB
-    if args.workload in DECODE_ONLY and args.bytes_per_gpu is None and not args.keep_size:
-        n = DECODE10G_BYTES
-    return False, n * world, rank * n, n, n
+    strong = total > 0
+    if not strong:
+        n = args.bytes_per_gpu if args.bytes_per_gpu is not None else GiB
+        if args.workload in DECODE_ONLY and args.bytes_per_gpu is None and not args.keep_size:
+            n = DECODE10G_BYTES
+        total = n * world
+    e2e = piece_step(unit, args.e2e_piece_bytes) if args.e2e_piece_bytes else default_e2e_piece(total, world, unit)
+    gp = piece_plan(total, world, rank, unit, e2e)
+    return strong, total, gp, sum(m for _, _, m in gp), e2e, pipeline_steps(total, world, unit, e2e)
 
 
 def main():
@@ -734,13 +777,13 @@ def main():
     decode_only = args.workload in DECODE_ONLY
     kind, seed, layout, chunk, desc = WORKLOADS[args.workload]
     unit = chunk if layout == snappy_amd.STREAMS else 65536
-    strong, total_in, r_off, n, n_max = resolve_sizes(args, world, rank)
+    strong, total_in, gpieces, n, e2e_piece, e2e_steps = resolve_sizes(args, world, rank)
     codec = snappy_amd.Codec(dev.index)
     codec.enable_timing(True)
     stream = torch.cuda.current_stream(dev)
     codec.set_stream(stream.cuda_stream)
     t_setup = time.perf_counter()
-    job = Job(args.workload, codec, dev, n, r_off, total_in, n_max, args.piece_bytes)
+    job = Job(args.workload, codec, dev, gpieces, total_in, args.piece_bytes, e2e_piece, e2e_steps)
     dcodec = None
     if args.overlap and not decode_only:
         dcodec = snappy_amd.Codec(dev.index)
@@ -782,7 +825,8 @@ def main():
 
     assemble = None
     if use_dist and not args.no_assemble and not decode_only:
-        assemble = end_to_end(job, world, rank, args, cdev, gloo, allgather, total_in)
+        meta = dist.group.WORLD if gloo else dist.new_group(backend="gloo")  # C1: host-side sizes
+        assemble = end_to_end(job, world, rank, args, cdev, gloo, allgather, total_in, meta)
         torch_peak = max(torch_peak, assemble.pop("torch_peak_bytes"))
         ok = ok and assemble["verified"]
         if args.c3:
@@ -794,8 +838,8 @@ def main():
     pmc = load_pmc(args.pmc, args.workload, job.n if decode_only else job.pieces[-1].n)
     config3 = strong and total_in == CONFIG3_BYTES and args.workload == "text32k"
     rep = kernel_report(job, clen, k1, k3, k4, pmc)
-    plan = rank_plan(total_in if strong else n * world, world, unit, args.piece_bytes,
-                     exchange=world > 1 and not args.no_assemble, gather_decoded=args.c3)
+    plan = rank_plan(total_in, world, unit, args.piece_bytes, exchange=world > 1 and not args.no_assemble,
+                     gather_decoded=args.c3, e2e_piece=e2e_piece, c2_max=args.c2_max_bytes)
     used = mem_after_steps[1] - mem_after_steps[0]
     rank_peak = torch_peak + scratch_peak
     n_units = job.units
@@ -880,99 +924,124 @@ def main():
         sys.exit(3)
 
 
-COMPACT_BOUNCE = 256 << 20  # dist.COMPACT_BOUNCE: the compaction's staging buffer
-
-
-def compact_in_place(full: torch.Tensor, mx: int, sz, offs, bounce: torch.Tensor) -> None:
-    """Move shard r of the padded C2 gather from r * mx down to its stream
-    offset offs[r] <= r * mx, in place: in ascending order, each piece staged
-    through `bounce` (a piece's destination can overlap its own source and
-    earlier pieces' sources, which were already read, never a later piece's),
-    so the gather buffer becomes the contiguous stream without a second
-    stream-sized buffer (dist.rank_plan)."""
-    step = bounce.numel()
-    for r in range(1, len(sz)):
-        src, dst = r * mx, int(offs[r])
-        if src == dst:
-            continue
-        for o in range(0, sz[r], step):
-            m = min(step, sz[r] - o)
-            if dst + o + m <= src + o:  # no overlap: one copy
-                full[dst + o:dst + o + m].copy_(full[src + o:src + o + m])
-            else:
-                bounce[:m].copy_(full[src + o:src + o + m])
-                full[dst + o:dst + o + m].copy_(bounce[:m])
-
-
-def end_to_end(job: Job, world: int, rank: int, args, cdev, gloo, allgather, total_in: int) -> dict:
-    """The whole job as one pipeline, timed over --e2e-steps steps (max over
-    ranks): compress the shard, C1 (size all-gather -> every shard's offset),
-    C2 (all-gather of the payloads padded to the largest: RCCL has no
-    all-gatherv), compaction of the padded gather into the contiguous stream
-    every rank then holds (byte-identical to a 1-GPU stream for SINGLE), and
-    decompress of this rank's blocks out of that stream.  Verified afterwards:
-    per-shard checksums of the reassembled stream and the round trip."""
+def end_to_end(job: Job, world: int, rank: int, args, cdev, gloo, allgather, total_in: int, meta) -> dict:
+    """The whole job as one pipeline, timed over --e2e-steps runs (max over
+    ranks).  The job is sharded block-cyclically (dist.piece_plan): step k
+    handles global pieces k*world .. k*world+world-1, one per rank.  Per step:
+      compress the rank's piece k (compute stream; returns its size),
+      C1  all-gather of the step's sizes over a host-side gloo group (so it
+          never queues behind the RCCL stream's C2),
+      C2  on the comm stream: RCCL all-gather of the step's payloads, padded
+          to the step's largest (RCCL has no all-gatherv), at most
+          --c2-max-bytes per rank per collective, into a gather buffer; then
+          each rank's part is copied to its offset in the reassembled stream
+          (known from the sizes: the step's pieces are a contiguous run of it),
+      decode of the rank's piece out of the stream (decode stream).
+    C2 and the decode of step k run while step k+1 compresses.  The stream
+    every rank ends with is byte-identical to a 1-GPU stream (SINGLE: one
+    snappy_compress() stream; STREAMS: the streams in order).  Verified
+    afterwards: the round trip and every global piece's checksum (its owner's
+    payload against its run of every rank's stream)."""
     dev = job.dev
-    sizes = torch.zeros(world, dtype=torch.int64, device=cdev)
-    state = {"full": None, "bounce": None, "mx": 0}
+    unit, chunk, layout = job.unit, job.chunk, job.layout
+    steps_k = job.steps_e2e
+    comp_stream = torch.cuda.current_stream(dev)
+    comm = torch.cuda.Stream(dev)
+    dstream = torch.cuda.Stream(dev)
+    dcodec = snappy_amd.Codec(dev.index)
+    dcodec.set_stream(dstream.cuda_stream)
+    overlap = not args.no_e2e_overlap
+    for gp in job.gpieces:
+        if gp.offs is None:
+            gp.offs = torch.empty(job.codec.num_units(gp.n, chunk, layout) + 1, dtype=torch.int64, device=dev)
+    # the reassembled stream: every global piece at its worst-case bound
+    g_all = [m for r in range(world) for _, _, m in piece_plan(total_in, world, r, unit, job.e2e_piece)]
+    stream_cap = sum(job.codec.max_output(m, chunk, layout) for m in g_all) + 16
+    stream = torch.empty(stream_cap, dtype=torch.uint8, device=dev)
+    cmax = max(1, min(job.slot, args.c2_max_bytes))
+    gbuf = torch.empty(world * cmax, dtype=torch.uint8, device=cdev)
+    sizes_log = []
 
-    def step():
-        clen = job.compress_all()
-        allgather(sizes, torch.tensor([clen], dtype=torch.int64, device=cdev))  # C1
-        sz = [int(v) for v in sizes.cpu()]
-        mx = max(max(sz), 1)
-        if state["full"] is None or state["full"].numel() < world * mx:
-            state["full"] = None
-            torch.cuda.empty_cache()
-            state["full"] = torch.empty(world * mx, dtype=torch.uint8, device=cdev)
-            state["bounce"] = torch.empty(COMPACT_BOUNCE, dtype=torch.uint8, device=cdev)
-        full, bounce = state["full"], state["bounce"]
-        state["mx"] = mx
-        if gloo:
-            allgather(full[:world * mx], job.out[:mx].to(cdev))
-        else:
-            allgather(full[:world * mx], job.out[:mx])  # C2 (job.out holds >= mx bytes on every rank)
-        offs = np.concatenate([[0], np.cumsum(sz)])
-        compact_in_place(full, mx, sz, offs, bounce)
-        stream = full[:int(offs[-1])]
-        if gloo:
-            stream = stream.to(dev)
-        state["stream"] = stream
-        job.decompress_all(stream.data_ptr() + int(offs[rank]))
-        return sz
+    def c1(clen: int):
+        t = torch.tensor([clen], dtype=torch.int64)
+        parts = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(parts, t, group=meta)
+        return [int(v) for v in parts]
 
-    step()  # untimed: allocates the gather buffers
-    torch.cuda.synchronize(dev)
+    def run():
+        base = 0
+        sizes_log.clear()
+        for k in range(steps_k):
+            gp = job.gpieces[k] if k < len(job.gpieces) else None
+            clen = 0
+            if gp is not None:
+                gp.clen = clen = job.codec.compress_ptr_ex(job.x.data_ptr() + gp.xoff, gp.n, chunk, layout,
+                                                           gp.flags, job.header_value,
+                                                           job.out.data_ptr() + k * job.slot, gp.offs.data_ptr())
+            sz = c1(clen)  # C1
+            sizes_log.append(sz)
+            comm.wait_stream(comp_stream)
+            with torch.cuda.stream(comm):  # C2 (a rank without a piece this step sends slot 0's bytes)
+                so = (k if gp is not None else 0) * job.slot
+                c2_gather_step(job.out[so:so + job.slot], sz, stream, base, gbuf)
+            if gp is not None:
+                dstream.wait_stream(comm)
+                dcodec.decompress_ptr_ex(stream.data_ptr() + base + int(sum(sz[:rank])), gp.offs.data_ptr(), gp.n,
+                                         chunk, layout, gp.flags, job.header_value, job.back.data_ptr() + gp.xoff,
+                                         check=False)
+            if not overlap:
+                torch.cuda.synchronize(dev)
+            base += sum(sz)
+        comp_stream.wait_stream(comm)
+        comp_stream.wait_stream(dstream)
+        torch.cuda.synchronize(dev)
+        return base
+
+    run()  # untimed: warms the communicators and the gather buffer
     dist.barrier()
-    steps = max(1, args.e2e_steps)
+    torch.cuda.synchronize(dev)
+    runs = max(1, args.e2e_steps)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        sz = step()
+    for _ in range(runs):
+        total_stream = run()
     torch.cuda.synchronize(dev)
     dist.barrier()
     tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=cdev)
     torch_peak = torch.cuda.max_memory_allocated(dev)  # before the checks' temporaries
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    t = float(tt) / steps
-    ok = job.verify()
-    # per-shard checksums: each rank's own payload against its slice of every rank's stream
-    mine = torch.tensor([checksum(job.out[:sz[rank]])], dtype=torch.int64, device=cdev)
-    sums = torch.zeros(world, dtype=torch.int64, device=cdev)
-    allgather(sums, mine)
-    offs = np.concatenate([[0], np.cumsum(sz)])
-    stream = state["stream"]
-    for r in range(world):
-        ok &= checksum(stream[offs[r]:offs[r] + sz[r]]) == int(sums[r])
+    t = float(tt) / runs
+    st = dcodec.decompress_status()
+    ok = st == 0 and all(bool(torch.equal(job.back[o:min(o + GiB, job.n)], job.x[o:min(o + GiB, job.n)]))
+                         for o in range(0, job.n, GiB))
+    # every global piece: its owner's payload checksum against its run of this rank's stream
+    mine = [checksum(job.out[gp.k * job.slot:gp.k * job.slot + gp.clen]) for gp in job.gpieces]
+    mine += [0] * (steps_k - len(mine))
+    sums = [torch.zeros(steps_k, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(sums, torch.tensor(mine, dtype=torch.int64), group=meta)
+    base = 0
+    for k, sz in enumerate(sizes_log):
+        for r in range(world):
+            if sz[r]:
+                ok &= checksum(stream[base:base + sz[r]]) == int(sums[r][k])
+            base += sz[r]
+    ok &= base == total_stream
+    if args.e2e_dump and rank == 0:
+        stream[:total_stream].cpu().numpy().tofile(args.e2e_dump)
     flag = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=cdev)
     dist.all_reduce(flag, op=dist.ReduceOp.MAX)
-    mx = state["mx"]
+    max_step = max(max(sz) for sz in sizes_log)
     res = {"value_end_to_end": round(total_in / t / 1e6, 1),
-           "end_to_end_ms_per_step": round(t * 1e3, 3), "end_to_end_steps": steps,
-           "end_to_end_step": "compress + C1 + C2 padded all-gather + compaction + decompress from the stream",
-           "stream_bytes": int(sum(sz)), "c2_padded_bytes_per_rank_out": world * mx,
+           "end_to_end_ms_per_step": round(t * 1e3, 3), "end_to_end_steps": runs,
+           "end_to_end_step": "per pipeline step: compress the rank's piece, C1 size all-gather, C2 all-gather of the "
+                              "step's payloads + copy into the reassembled stream, decode of the piece from the stream;"
+                              + (" C2 and decode overlap the next step's compress" if overlap else " serialised (A/B)"),
+           "sharding": f"block-cyclic, global pieces of {job.e2e_piece} B, {steps_k} pipeline steps per rank",
+           "stream_bytes": int(total_stream), "c2_padded_bytes_per_rank_in": int(sum(world * max(sz) for sz in sizes_log)),
+           "c2_largest_collective_bytes_per_rank": int(min(max_step, cmax)),
            "backend": "gloo" if gloo else "nccl (RCCL)", "verified": float(flag) == 0.0,
            "torch_peak_bytes": torch_peak}
-    state["full"] = state["stream"] = state["bounce"] = None
+    dcodec.close()
+    del stream, gbuf
     torch.cuda.empty_cache()
     return res
 

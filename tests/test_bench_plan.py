@@ -16,25 +16,57 @@ import snappy_amd  # noqa: E402
 GiB = 1 << 30
 
 
+def _sizes(a, world, rank):
+    strong, total, gp, n, e2e, steps = bench.resolve_sizes(a, world, rank)
+    return strong, total, n, e2e, steps, gp
+
+
 def test_default_sizes():
     a = bench.parse([])
-    # configs[3] at every N: the N = 1 point is the same 64 GiB job (one curve)
-    assert bench.resolve_sizes(a, 1, 0) == (True, 64 * GiB, 0, 64 * GiB, 64 * GiB)
+    # configs[3] at every N: the N = 1 point is the same 64 GiB job (one curve), in 1 GiB pieces
+    assert _sizes(a, 1, 0)[:5] == (True, 64 * GiB, 64 * GiB, GiB, 64)
     a1 = bench.parse(["--bytes-per-gpu", str(GiB)])  # configs[1] alone
-    assert bench.resolve_sizes(a1, 1, 0) == (False, GiB, 0, GiB, GiB)
+    assert _sizes(a1, 1, 0)[:3] == (False, GiB, GiB)
     a2 = bench.parse(["--workload", "text64k"])  # another workload alone at N = 1: 1 GiB
-    assert bench.resolve_sizes(a2, 1, 0) == (False, GiB, 0, GiB, GiB)
-    assert bench.resolve_sizes(a2, 2, 1)[:2] == (True, 64 * GiB)
-    for world in (2, 4, 8):  # configs[3]: 64 GiB strong-scaled
-        strong, total, off, n, n_max = bench.resolve_sizes(a, world, world - 1)
-        assert strong and total == 64 * GiB and n == n_max == 64 * GiB // world
-        assert off == (world - 1) * n
+    assert _sizes(a2, 1, 0)[:3] == (False, GiB, GiB)
+    assert _sizes(a2, 2, 1)[:2] == (True, 64 * GiB)
+    for world in (2, 4, 8):  # configs[3]: 64 GiB strong-scaled, block-cyclic 1 GiB pieces
+        strong, total, n, e2e, steps, gp = _sizes(a, world, world - 1)
+        assert strong and total == 64 * GiB and n == 64 * GiB // world and e2e == GiB
+        assert steps == 64 // world and [g for g, _, _ in gp] == list(range(world - 1, 64, world))
     a = bench.parse(["--weak"])
-    assert bench.resolve_sizes(a, 2, 1) == (False, 2 * GiB, GiB, GiB, GiB)
+    strong, total, n, e2e, steps, gp = _sizes(a, 2, 1)
+    assert (strong, total, n) == (False, 2 * GiB, GiB) and e2e * 2 * steps == total
     a = bench.parse(["--total-bytes", str(64 * GiB)])  # the N = 1 point of configs[3]
-    assert bench.resolve_sizes(a, 1, 0) == (True, 64 * GiB, 0, 64 * GiB, 64 * GiB)
+    assert _sizes(a, 1, 0)[:3] == (True, 64 * GiB, 64 * GiB)
     a = bench.parse(["--workload", "decode10g"])
-    assert bench.resolve_sizes(a, 1, 0)[3] == bench.DECODE10G_BYTES
+    assert _sizes(a, 1, 0)[2] == bench.DECODE10G_BYTES
+
+
+@pytest.mark.parametrize("total,world,unit", [(64 * GiB, 8, 32768), (200 * 65536 + 12345, 2, 65536),
+                                              (5 * 65536, 8, 65536), (1, 3, 65536), (0, 2, 32768),
+                                              (256 << 20, 8, 32768), (18_499_960_832, 1, 65536)])
+def test_piece_plan_covers(total, world, unit):
+    """Block-cyclic pieces: every byte once, unit-aligned, piece g on rank g
+    mod world (rank 0 holds global offset 0), each pipeline step one piece
+    per rank at most."""
+    e2e = sdist.default_e2e_piece(total, world, unit)
+    assert e2e % unit == 0 and e2e <= GiB
+    plans = [sdist.piece_plan(total, world, r, unit, e2e) for r in range(world)]
+    allp = sorted(x for p in plans for x in p)
+    pos = 0
+    for g, off, n in allp:
+        assert off == pos and off % unit == 0 and n > 0
+        pos += n
+    assert pos == total
+    for r, p in enumerate(plans):
+        assert all(g % world == r for g, _, _ in p)
+        assert len(p) <= sdist.pipeline_steps(total, world, unit, e2e)
+    if total:
+        assert plans[0][0][1] == 0
+    # a share of whole units is split into equal pieces (weak scaling: equal shares)
+    if total % (world * unit) == 0 and total:
+        assert len({n for _, _, n in allp}) == 1 or e2e == sdist.piece_step(unit, min(GiB, total // world // 4))
 
 
 @pytest.mark.parametrize("world", [1, 2, 4, 8])
@@ -45,7 +77,9 @@ def test_rank_plan_fits_hbm(world):
     p = sdist.rank_plan(64 * GiB, world, 32768, a.piece_bytes, exchange=True, gather_decoded=True)
     assert p["peak"] < sdist.HBM_BYTES, p
     if world > 1:
-        assert "c2_gather_buffer" in p and "c3_phase_peak" in p
+        assert "c2_stream" in p and "c2_gather_buffer" in p and "c3_phase_peak" in p
+        # the reassembled stream holds the whole job (worst case), the gather buffer one collective per rank
+        assert p["c2_stream"] >= sdist.max_output(64 * GiB, 32768) and p["c2_gather_buffer"] <= world * (1 << 30)
 
 
 def test_plan_matches_library_bounds():

@@ -84,6 +84,61 @@ def test_sharded_stream_identical(world, n):
     assert all(k == units + 1 for _, _, k in res)
 
 
+def _pipeline_worker(rank, world, port, n, piece, cmax, q):
+    """One rank of bench.py's end-to-end pipeline on the CPU: block-cyclic
+    pieces (dist.piece_plan) compressed by the oracle stand-in, per step C1
+    (sizes) and C2 (dist.c2_gather_step over gloo, host buffers) into the
+    stream every rank holds."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import dist as sdist
+        a = datagen.make("T", n, 79)
+        mine = sdist.piece_plan(n, world, rank, BLOCK, piece)
+        steps = sdist.pipeline_steps(n, world, BLOCK, piece)
+        slot = sdist.max_output(piece, BLOCK)
+        stream = torch.zeros(sum(sdist.max_output(m, BLOCK) for r in range(world)
+                                 for _, _, m in sdist.piece_plan(n, world, r, BLOCK, piece)) + 16, dtype=torch.uint8)
+        gbuf = torch.empty(world * cmax, dtype=torch.uint8)
+        base = 0
+        for k in range(steps):
+            src = torch.full((slot,), 0xAB, dtype=torch.uint8)  # padding a gather must never place
+            clen = 0
+            if k < len(mine):
+                g, off, m = mine[k]
+                payload, _ = shard_compress(a[off:off + m], n, off == 0)
+                clen = len(payload)
+                src[:clen] = torch.frombuffer(bytearray(payload), dtype=torch.uint8)
+            sizes = sdist.exchange_sizes(clen, torch.device("cpu"))
+            sdist.c2_gather_step(src, sizes, stream, base, gbuf)
+            base += sum(sizes)
+        q.put((rank, stream[:base].numpy().tobytes() == oracle.compress(a.tobytes())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,piece,cmax", [(2, 9 * BLOCK + 77, 2 * BLOCK, 1 << 20),
+                                                (3, 20 * BLOCK, 2 * BLOCK, 5000),
+                                                (8, 21 * BLOCK + 77, BLOCK, 30000),
+                                                (4, 3 * BLOCK, 2 * BLOCK, 1 << 20)])
+def test_pipelined_c2_stream_identical(world, n, piece, cmax):
+    """bench.py's pipelined C2 (block-cyclic pieces, one all-gather per step,
+    split into collectives of at most cmax bytes per rank, ranks without a
+    piece in the last step) reassembles exactly the whole-input reference
+    stream on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, world, port, n, piece, cmax, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(60)
+    assert all(ok for _, ok in res), res
+
+
 def test_shard_range_covers():
     import dist as sdist
     for n in (0, 1, BLOCK, 10 * BLOCK + 5, 123456789):
@@ -183,16 +238,52 @@ def test_bench_spawns_ranks_weak():
 
 
 @pytest.mark.gpu
-def test_bench_strong_pieces():
+def test_bench_strong_pieces(tmp_path):
     """--total-bytes fixes the job (strong scaling); --piece-bytes splits a
-    rank's range into several compress calls, SINGLE layout (one stream)."""
+    rank's pieces into several compress calls, SINGLE layout (one stream).
+    The end-to-end pipeline (block-cyclic pieces of 25 blocks, 5 steps, the
+    last with one rank idle) reassembles exactly the reference's stream of
+    the whole input on rank 0."""
+    total = 100 * BLOCK * 2 + 12345
+    dump = str(tmp_path / "stream.snp")
     d = _bench("--gpus", "2", "--dist-backend", "gloo", "--workload", "text64k", "--total-bytes",
-               str(100 * BLOCK * 2 + 12345), "--piece-bytes", str(40 * BLOCK), "--steps", "2", "--warmup", "1",
-               "--no-host-e2e")
+               str(total), "--piece-bytes", str(40 * BLOCK), "--steps", "2", "--warmup", "1",
+               "--no-host-e2e", "--e2e-dump", dump)
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["round_trip_ok"]
     assert d["config"]["pieces_per_gpu"] == 3 and d["exchange"]["verified"]
-    # the reassembled SINGLE stream: every byte once, in order
-    assert d["exchange"]["stream_bytes"] > 0
+    got = open(dump, "rb").read()
+    assert d["exchange"]["stream_bytes"] == len(got)
+    assert got == oracle.compress(datagen.make("T", total, 1234).tobytes())
+
+
+@pytest.mark.gpu
+def test_bench_rccl_world1_large_collective(tmp_path):
+    """RCCL at configs[3]'s real counts: a 1-rank communicator whose C2 sends
+    one all-gather of more than 2^32 bytes (5 GiB of random bytes in one
+    piece, payload ~5.4 GB, --c2-max-bytes above it).  The reassembled
+    stream's checksums and the round trip are verified by bench.py."""
+    n = 5 << 30
+    d = _bench("--dist-world1", "--dist-backend", "nccl", "--workload", "random", "--bytes-per-gpu", str(n),
+               "--e2e-piece-bytes", str(n), "--c2-max-bytes", str(8 << 30), "--steps", "1", "--warmup", "0",
+               "--e2e-steps", "1", "--no-host-e2e", "--no-cpu-baseline", "--no-sub")
+    ex = d["exchange"]
+    assert d["round_trip_ok"] and ex["verified"] and ex["backend"].startswith("nccl")
+    assert ex["c2_largest_collective_bytes_per_rank"] > 1 << 32
+    assert ex["stream_bytes"] > n  # random bytes: every block stored as literals
+
+
+@pytest.mark.gpu
+def test_bench_gloo_world2_large_payload():
+    """gloo world 2 (ranks sharing the GPU) with a per-rank payload above
+    2^32 bytes sent as one collective: 9 GiB of random bytes, one 4.5 GiB
+    piece per rank (payload ~4.8 GB each).  Shard checksums and the round
+    trip are verified on both ranks."""
+    d = _bench("--gpus", "2", "--dist-backend", "gloo", "--workload", "random", "--total-bytes", str(9 << 30),
+               "--e2e-piece-bytes", str(9 << 29), "--c2-max-bytes", str(8 << 30), "--steps", "1", "--warmup", "0",
+               "--e2e-steps", "1", "--no-host-e2e")
+    ex = d["exchange"]
+    assert d["round_trip_ok"] and ex["verified"]
+    assert ex["c2_largest_collective_bytes_per_rank"] > 1 << 32
 
 
 @pytest.mark.gpu
@@ -218,10 +309,11 @@ def test_bench_memory_within_plan(world):
 def test_bench_world8_rehearsal():
     """configs[3]'s 8-rank path on the one GPU of a box: bench.py --gpus 8
     spawns 8 ranks (torch.distributed.run, gloo collectives, all ranks on
-    cuda:0) of a 256 MiB strong-scaled job in 16 MiB pieces -- C1 in every
-    step, the end-to-end loop with the C2 gather compacted in place into the
-    stream, per-shard checksums and the round trip verified on every rank,
-    and every rank's measured peak within dist.rank_plan for that size."""
+    cuda:0) of a 256 MiB strong-scaled job (block-cyclic 8 MiB pieces, four
+    pipeline steps per rank, compress launches of 16 MiB) -- C1 in every
+    step, the overlapped end-to-end pipeline (C2 per step into the stream,
+    decode from it), per-piece checksums and the round trip verified on
+    every rank, and every rank's measured peak within dist.rank_plan."""
     total = 256 << 20
     d = _bench("--gpus", "8", "--dist-backend", "gloo", "--total-bytes", str(total), "--piece-bytes", str(16 << 20),
                "--steps", "1", "--warmup", "1", "--no-host-e2e")
@@ -229,6 +321,7 @@ def test_bench_world8_rehearsal():
     assert d["config"]["total_bytes"] == total and d["config"]["bytes_per_gpu"] == total // 8
     assert d["config"]["pieces_per_gpu"] == 2
     assert d["exchange"]["verified"] and d["value_end_to_end"] > 0
+    assert "4 pipeline steps" in d["exchange"]["sharding"]
     m = d["memory"]
     assert 0 < m["rank_peak_bytes"] <= m["planned_peak_bytes_per_rank"], m
 

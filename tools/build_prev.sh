@@ -17,11 +17,13 @@ mkdir -p $P/variants $P/build
 # shim launches the kernels with REV's signatures); the C host from the tree
 D=$P/build/src_$NAME
 rm -rf $D && mkdir -p $D
-for f in snappy_kernels.hip snappy_kernels.h snappy_device.hip; do
+# (from round 5 the shim's host pipelines are snappy_pipeline.cpp + snappy_ctx.h;
+# older revisions hold them in snappy_device.hip, so those two may be absent)
+for f in snappy_kernels.hip snappy_kernels.h snappy_device.hip snappy_ctx.h snappy_pipeline.cpp; do
     case $REV in
-    WORK) cp $P/csrc/$f $D/$f ;;
-    DIR:*) cp ${REV#DIR:}/$f $D/$f ;;  # a directory holding the three files
-    *) git show $REV:$P/csrc/$f > $D/$f ;;
+    WORK) [ -f $P/csrc/$f ] && cp $P/csrc/$f $D/$f ;;
+    DIR:*) [ -f ${REV#DIR:}/$f ] && cp ${REV#DIR:}/$f $D/$f ;;  # a directory holding the files
+    *) git show $REV:$P/csrc/$f > $D/$f 2>/dev/null || rm -f $D/$f ;;
     esac
 done
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=${VARCH:-gfx950} -mcode-object-version=5 -Iinclude -I$D $*"
@@ -31,7 +33,13 @@ hipcc $FLAGS $SC -DSNAPPY_TU=1 -x hip -c $D/snappy_kernels.hip -o $P/build/kc_$N
 hipcc $FLAGS $SD -DSNAPPY_TU=2 -x hip -c $D/snappy_kernels.hip -o $P/build/kd_$NAME.o
 hipcc -O3 -std=c++17 -fPIC --offload-arch=${VARCH:-gfx950} -mcode-object-version=5 -Iinclude -I$D -c $D/snappy_device.hip -o $P/build/dev_$NAME.o
 gcc -O2 -fPIC -std=gnu11 -Iinclude -c $P/csrc/snappy_host.c -o $P/build/host_var.o
+PIPE=""
+if [ -f $D/snappy_pipeline.cpp ]; then
+    g++ -O2 -std=c++17 -fPIC -pthread -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -I$D \
+        -c $D/snappy_pipeline.cpp -o $P/build/pipe_$NAME.o
+    PIPE=$P/build/pipe_$NAME.o
+fi
 hipcc --offload-arch=${VARCH:-gfx950} -shared -fPIC -o $P/variants/libsnappy_amd_$NAME.so $P/build/kc_$NAME.o $P/build/kd_$NAME.o \
-    $P/build/dev_$NAME.o $P/build/host_var.o
+    $P/build/dev_$NAME.o $PIPE $P/build/host_var.o
 rm -rf $D
 echo "built $NAME ($REV $*)"

@@ -174,6 +174,14 @@ for step in "$@"; do
         SNAPPY_AMD_LIB=$PWD/lightweight-snappy_amd/variants/libsnappy_amd_$v.so timeout -k 10 700 \
             python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > "$out/gpu_tests_$v.log" 2>&1
         rc=$?; echo "testsv $v rc=$rc"; tail -3 "$out/gpu_tests_$v.log"; fatal $rc && exit $rc ;;
+    e2e:*)  # e2e:<total bytes> -> end-to-end pipeline over a 1-rank RCCL communicator, overlapped vs serialised, twice
+        tb=${step#e2e:}
+        for r in 1 2; do for o in "" "--no-e2e-overlap"; do
+            timeout -k 10 400 python -u bench.py --dist-world1 --total-bytes $tb --steps 2 --warmup 1 --e2e-steps 2 \
+                --no-sub --no-cpu-baseline --no-host-e2e $o >> "$out/e2e_$tb.json" 2>> "$out/e2e_$tb.err"
+            rc=$?; echo "e2e '$o' rc=$rc"; [ $rc -ne 0 ] && exit $rc
+        done; done
+        python3 -c "import json,sys; [print(d['ms_per_step'], d['value'], d['value_end_to_end'], d['exchange']['end_to_end_ms_per_step'], d['exchange']['end_to_end_step'][-40:], d['round_trip_ok']) for d in map(json.loads, [l for l in open(sys.argv[1]) if l.startswith('{')])]" "$out/e2e_$tb.json" ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -29,6 +29,8 @@ struct snappy_amd_ctx {
     int32_t *h_status = nullptr;    // pinned, grows with status_cap
     size_t h_status_cap = 0;
     size_t last_units = 0;
+    bool status_pending = false;    // the last decode's status words not read back yet
+    int last_status = 0;            // its result once read (decompress_status returns it again)
     int last_layout = SNAPPY_AMD_SINGLE;  // of the last decode launch (status mapping)
     // host-buffer path staging
     uint8_t *d_a = nullptr; size_t d_a_cap = 0;

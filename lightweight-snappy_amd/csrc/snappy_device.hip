@@ -91,15 +91,15 @@ int snappy_amd_trim(snappy_amd_ctx *c)
         {reinterpret_cast<void **>(&c->d_a), &c->d_a_cap}, {reinterpret_cast<void **>(&c->d_b), &c->d_b_cap},
         {reinterpret_cast<void **>(&c->d_idx), &c->d_idx_cap}, {reinterpret_cast<void **>(&c->k5buf), &c->k5buf_cap},
         {reinterpret_cast<void **>(&c->k5copy), &c->k5copy_cap},
-        // a decode's status words only until its status has been read
-        {reinterpret_cast<void **>(&c->status), c->last_units ? nullptr : &c->status_cap}};
+        // a decode's status words only once its status has been read (the result is kept)
+        {reinterpret_cast<void **>(&c->status), c->status_pending ? nullptr : &c->status_cap}};
     for (auto &b : bufs) {
         if (!b.cap) continue;
         if (*b.p) (void)hipFree(*b.p);
         *b.p = nullptr;
         *b.cap = 0;
     }
-    if (!c->last_units && c->h_status) {
+    if (!c->status_pending && c->h_status) {
         (void)hipHostFree(c->h_status);
         c->h_status = nullptr;
         c->h_status_cap = 0;
@@ -273,6 +273,8 @@ static int decompress_launch(snappy_amd_ctx *c, const void *d_comp, const uint64
     if (unit == 0 || unit > SNAPPY_AMD_BLOCK) return SNAPPY_AMD_ERR_ARG;
     HIP_OK(hipSetDevice(c->device));
     c->last_units = 0;
+    c->status_pending = false;
+    c->last_status = SNAPPY_AMD_OK;
     if (n == 0) return SNAPPY_AMD_OK;
     const size_t units = (n + unit - 1) / unit;
     if (units > 0xFFFFFFFFull) return SNAPPY_AMD_ERR_ARG;
@@ -306,13 +308,14 @@ static int decompress_launch(snappy_amd_ctx *c, const void *d_comp, const uint64
     }
     c->last_units = units;
     c->last_layout = layout;
+    c->status_pending = true;
     return SNAPPY_AMD_OK;
 }
 
 int snappy_amd_decompress_status(snappy_amd_ctx *c)
 {
     if (!c) return SNAPPY_AMD_ERR_ARG;
-    if (c->last_units == 0) return SNAPPY_AMD_OK;
+    if (!c->status_pending) return c->last_status;  // (read before, or no decode since)
     HIP_OK(hipSetDevice(c->device));
     const size_t bytes = c->last_units * sizeof(int32_t);
     if (bytes > c->h_status_cap) {
@@ -325,15 +328,17 @@ int snappy_amd_decompress_status(snappy_amd_ctx *c)
     HIP_OK(hipMemcpyAsync(c->h_status, c->status, bytes, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
     if (c->timing && c->ev_decode) (void)hipEventElapsedTime(&c->k4_ms, c->ev[3], c->ev[4]);
-    for (size_t i = 0; i < c->last_units; i++) {
+    int r = SNAPPY_AMD_OK;
+    for (size_t i = 0; i < c->last_units && r == SNAPPY_AMD_OK; i++) {
         // DEFER survives a STREAMS launch (no pass 2) only for a copy reaching
         // before the start of its own stream; after a SINGLE launch pass 2 ends
         // every deferred unit, so a DEFER left over is an internal failure
-        if (c->h_status[i] > 0) return c->last_layout == SNAPPY_AMD_STREAMS ? SNAPPY_AMD_ERR_OFFSET
-                                                                            : SNAPPY_AMD_ERR_DEVICE;
-        if (c->h_status[i] != SNAPPY_ST_OK) return c->h_status[i];
+        if (c->h_status[i] > 0) r = c->last_layout == SNAPPY_AMD_STREAMS ? SNAPPY_AMD_ERR_OFFSET : SNAPPY_AMD_ERR_DEVICE;
+        else if (c->h_status[i] != SNAPPY_ST_OK) r = c->h_status[i];
     }
-    return SNAPPY_AMD_OK;
+    c->last_status = r;
+    c->status_pending = false;
+    return r;
 }
 
 int snappy_amd_decompress_device_async(snappy_amd_ctx *c, const void *d_comp, const uint64_t *d_offsets, size_t n,

@@ -22,6 +22,7 @@
 #define SNAPPY_ST_CAPACITY (-6)
 #define SNAPPY_ST_UNSUPPORTED (-9)
 #define SNAPPY_ST_TIMEOUT (-10)   // K4 pass 2: a unit waited too long for an earlier one
+#define SNAPPY_ST_INDEX (-11)     // K4 (SINGLE): the unit's element chain does not end at the next index entry
 #define SNAPPY_ST_DEFER 2         // K4 pass 1: the unit copies from earlier units (pass 2 decodes it;
                                   // meanwhile its status is DEFER + output bytes already in HBM)
 

@@ -2417,6 +2417,14 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     }
 #undef WADR
 #undef WDW
+    // SINGLE: a unit whose last element ends inside it (skip1 == 0) must end
+    // exactly at the next entry.  Block 0 starts after the checked preamble,
+    // so by induction every entry of an index that passes is a true element
+    // boundary (and a straddle entry is tied to the chain by the tail check
+    // above): a sidecar entry moved inside an element is refused here instead
+    // of decoding a shifted block.  The last unit may leave bytes unread, as
+    // the reference does (src/snappy_decompression.c:356-359 stops at N).
+    if (st == SNAPPY_ST_OK && allow_back && !skip1 && base + unit < n && ip != clen) st = SNAPPY_ST_INDEX;
 #ifdef SNAPPY_K4_STATS
     if (lane == 0 && u < 32768) {
         uint64_t *g = g_k4_stats + 8 * u;

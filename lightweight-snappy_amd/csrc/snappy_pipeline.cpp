@@ -582,8 +582,10 @@ int host_compress_stage(HostCtx &h, const uint8_t *in, size_t n, uint32_t flags,
     return compress_impl(c, c->d_a, n, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE, flags, header_value, c->d_b, c->d_idx, len);
 }
 
-// a sidecar index must describe the stream: every entry inside it, never
-// decreasing, the last one its length (a tampered .idx is refused here)
+// a sidecar index's shape: one entry per block + the end, every entry inside
+// the stream, never decreasing, the last one its length (refused before any
+// copy to HBM); that the entries are the stream's element boundaries is
+// checked by the decode itself (K4 + sidecar_verdict)
 bool index_fits(const uint64_t *idx, size_t count, size_t units, uint64_t clen)
 {
     const uint64_t off_mask = (1ull << SNAPPY_AMD_IDX_OFFSET_BITS) - 1;
@@ -591,6 +593,24 @@ bool index_fits(const uint64_t *idx, size_t count, size_t units, uint64_t clen)
     for (size_t i = 0; i < units; i++)
         if ((idx[i] & off_mask) > (idx[i + 1] & off_mask)) return false;
     return true;
+}
+
+// A decode driven by a sidecar index failed (rc): it is the index's fault when
+// it is not the stream's own block index.  K4 refuses (SNAPPY_AMD_ERR_INDEX) a
+// SINGLE unit whose element chain does not end at the next entry, so a decode
+// that succeeds had the stream's own index; a failing one is settled here by
+// building that index (K5p) and comparing: a different sidecar -> ERR_INDEX,
+// the same -> the stream's error, exactly what the decode without a sidecar
+// reports (the index pass's own error when the stream cannot be indexed).
+int sidecar_verdict(snappy_amd_ctx *c, const uint8_t *d_stream, size_t n, const uint64_t *idx, size_t count, int rc)
+{
+    if (rc == SNAPPY_AMD_OK || rc == SNAPPY_AMD_ERR_DEVICE) return rc;
+    size_t got = 0;
+    int r = snappy_amd_index_device(c, d_stream, n, c->d_idx, count, &got);
+    if (r) return r;
+    std::vector<uint64_t> own(count);
+    HIP_OK(hipMemcpy(own.data(), c->d_idx, count * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return memcmp(own.data(), idx, count * sizeof(uint64_t)) ? SNAPPY_AMD_ERR_INDEX : rc;
 }
 
 // the largest output a valid stream of n compressed bytes can declare: a
@@ -655,6 +675,19 @@ int host_compress_pipelined(HostCtx &h, const uint8_t *in, size_t n, uint64_t he
             }
             high_priority_stream(h.pipe[i]);
         }
+    // on an error return, no lane may still be copying from `in` (the caller
+    // may free it) or be busy when the context goes back to the pool
+    struct LaneGuard {
+        HostCtx &h;
+        int lanes;
+        bool armed = true;
+        ~LaneGuard()
+        {
+            if (armed)
+                for (int i = 0; i < lanes; i++)
+                    if (h.pipe[i]) (void)hipStreamSynchronize(h.pipe[i]->stream);
+        }
+    } guard{h, lanes};
     size_t off = 0;  // compressed bytes placed so far
     auto drain = [&](size_t k) -> int {
         snappy_amd_ctx *c = h.pipe[k % (size_t)lanes];
@@ -684,6 +717,7 @@ int host_compress_pipelined(HostCtx &h, const uint8_t *in, size_t n, uint64_t he
     }
     for (size_t k = nch > (size_t)lanes ? nch - (size_t)lanes : 0; k < nch; k++)
         if ((rc = drain(k))) return rc;
+    guard.armed = false;  // (every lane drained)
     *out_len = off;
     return SNAPPY_AMD_OK;
 }
@@ -827,6 +861,7 @@ int snappy_amd_host_decompress_idx(const uint8_t *in, size_t n, const uint64_t *
     }
     if (N == 0) { *out_len = 0; return SNAPPY_AMD_OK; }
     rc = snappy_amd_decompress_device(c, c->d_a, c->d_idx, (size_t)N, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE, c->d_b);
+    if (rc && idx) rc = sidecar_verdict(c, c->d_a, n, idx, count, rc);
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(out, c->d_b, N, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
@@ -924,9 +959,9 @@ int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count
         pre.ok = true;
         return SNAPPY_AMD_OK;
     }
-    if ((rc = snappy_amd_decompress_device(c, c->d_a, c->d_idx, (size_t)N, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE,
-                                           c->d_b)))
-        return rc;
+    rc = snappy_amd_decompress_device(c, c->d_a, c->d_idx, (size_t)N, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE, c->d_b);
+    if (rc && idx) rc = sidecar_verdict(c, c->d_a, n, idx, count, rc);
+    if (rc) return rc;
     // (3) HBM -> pinned chunk (copy engine) -> file (a writer thread, itself
     // using several threads on a mapped output)
     const double t2 = io_now();
@@ -1133,9 +1168,13 @@ int snappy_decompress_buffer_multi(const int *devices, int ndev, const uint8_t *
                 e = SNAPPY_AMD_ERR_DEVICE;
             rcs[(size_t)r] = e;
         });
+        // the first failing range in order decides, as the first failing unit
+        // does for one device: ERR_OFFSET from a range after the first may be a
+        // legal copy from an earlier range, so the whole stream is decoded on
+        // one device (which then reports whatever error comes first)
         bool again = false;
-        for (int r = 0; r < parts; r++) {
-            if (rcs[(size_t)r] == SNAPPY_AMD_ERR_OFFSET && r > 0) again = true;  // copies from an earlier range
+        for (int r = 0; r < parts && !again; r++) {
+            if (rcs[(size_t)r] == SNAPPY_AMD_ERR_OFFSET && r > 0) again = true;
             else if (rcs[(size_t)r]) return rcs[(size_t)r];
         }
         if (!again) {

@@ -706,6 +706,15 @@ def test_tampered_sidecar_index_refused(codec):
     with pytest.raises(snappy_amd.SnappyError) as ei:  # trailing bytes / short file
         snappy_amd.decompress_indexed(stream, _index_file(a.size, ent) + b"\0")
     assert ei.value.code == snappy_amd.ERR_INDEX
+    # well-formed (in bounds, monotone) but not the stream's element boundaries:
+    # an entry moved one byte into an element, either way, in the middle or at
+    # the last block, is refused as ERR_INDEX, never decoded into other bytes
+    for k, d in ((1, 1), (1, -1), (20, 1), (20, -1), (len(ent) - 2, 1), (len(ent) - 2, -1)):
+        bad = list(ent)
+        bad[k] += d
+        with pytest.raises(snappy_amd.SnappyError) as ei:
+            snappy_amd.decompress_indexed(stream, _index_file(a.size, bad))
+        assert ei.value.code == snappy_amd.ERR_INDEX, (k, d)
     with pytest.raises(snappy_amd.SnappyError) as ei:
         snappy_amd.read_index(b"SNPA")
     assert ei.value.code == snappy_amd.ERR_INDEX
@@ -725,6 +734,13 @@ def test_device_index_past_stream_end_fails_cleanly(codec):
         codec.decompress_tensor(comp, bad, a.size, layout=snappy_amd.SINGLE)
     back = codec.decompress_tensor(comp, offs, a.size, layout=snappy_amd.SINGLE)
     assert torch.equal(back, x)
+    # an entry moved forward inside an element: K4 itself refuses it (the
+    # previous block's chain does not end there)
+    bad = offs.clone()
+    bad[5] += 1
+    with pytest.raises(snappy_amd.SnappyError) as ei:
+        codec.decompress_tensor(comp, bad, a.size, layout=snappy_amd.SINGLE)
+    assert ei.value.code == snappy_amd.ERR_INDEX
 
 
 @pytest.mark.parametrize("chunk", [17, 4095, 32768, 65535, 65536])
@@ -1030,6 +1046,28 @@ def test_multi_device_buffer_api(golden):
         assert len(out) == v["out_len"] and sha(out) == v["out_sha256"], v["name"]
     with pytest.raises(snappy_amd.SnappyError):
         snappy_amd.decompress_multi(want[:-3], [0, 0])
+    # malformed streams (bytes flipped in the later ranges): the same outcome --
+    # error code, or bytes -- as the one-device decode, whichever range fails first
+    rng = np.random.default_rng(75)
+    data = datagen.make("T", 9 << 20, 76).tobytes()
+    base = oracle.compress(data)
+
+    def outcome(f, b):
+        try:
+            return f(b)
+        except snappy_amd.SnappyError as e:
+            return e.code
+
+    codes = set()
+    for t in range(12):
+        bad = bytearray(base)
+        for p in rng.integers(len(base) // 4, len(base), 1 + t % 3):
+            bad[int(p)] ^= int(rng.integers(1, 256))
+        bad = bytes(bad)
+        one = outcome(snappy_amd.decompress, bad)
+        codes.add(one if isinstance(one, int) else 0)
+        assert outcome(lambda b: snappy_amd.decompress_multi(b, [0, 0, 0]), bad) == one, t
+    assert len(codes) > 1, codes  # the corruptions reach more than one kind of outcome
 
 
 def test_decompress_file_bogus_length():

@@ -249,7 +249,7 @@ def cpu_reference(kind: str, seed: int, chunk: int, layout: int, sample: int, de
                       f"{a.size / (t2 - t1) / 1e6:.1f} MB/s, reference src/*.c -O2 through its FILE* API (tmpfiles)"}
 
 
-def host_end_to_end(kind: str, seed: int, sample: int) -> dict:
+def host_end_to_end(kind: str, seed: int, sample: int, runs: int = 5) -> dict:
     """PCIe-inclusive rate of the drop-in host API (snappy_compress_buffer /
     snappy_decompress_buffer: one SINGLE stream of 64 KiB blocks, pageable
     host buffers in and out).  Reported beside `value`, never as it."""
@@ -260,8 +260,8 @@ def host_end_to_end(kind: str, seed: int, sample: int) -> dict:
     back = np.empty(a.size, dtype=np.uint8)
     got = ctypes.c_size_t(0)
     vp = ctypes.c_void_p
-    best_c = best_d = float("inf")
-    for _ in range(3):
+    tc, td = [], []
+    for _ in range(1 + runs):  # the first call also allocates the pipeline's contexts: untimed
         t0 = time.perf_counter()
         rc = lib.snappy_compress_buffer(vp(a.ctypes.data), a.size, vp(comp.ctypes.data), ctypes.byref(got))
         t1 = time.perf_counter()
@@ -271,13 +271,22 @@ def host_end_to_end(kind: str, seed: int, sample: int) -> dict:
                                           ctypes.byref(got))
         t2 = time.perf_counter()
         assert rc == 0 and got.value == a.size, rc
-        best_c, best_d = min(best_c, t1 - t0), min(best_d, t2 - t1)
+        tc.append(t1 - t0)
+        td.append(t2 - t1)
     assert np.array_equal(back, a)
-    return {"bytes": int(a.size), "layout": "SINGLE 64 KiB blocks", "compress_MBps": round(a.size / best_c / 1e6, 1),
-            "decompress_MBps": round(a.size / best_d / 1e6, 1), "note": "pageable host buffers, H2D+D2H included"}
+    return dict({"bytes": int(a.size), "layout": "SINGLE 64 KiB blocks",
+                 "note": f"pageable host buffers, H2D+D2H included; median of {runs} timed runs after one untimed"},
+                **rate_stats(a.size, tc[1:], "compress"), **rate_stats(a.size, td[1:], "decompress"))
 
 
-def host_file_api(nbytes: int) -> dict:
+def rate_stats(nbytes: int, times, what: str) -> dict:
+    """{what}_MBps (the median run) and its min / max over the runs."""
+    r = sorted(nbytes / t / 1e6 for t in times)
+    return {f"{what}_MBps": round(float(np.median(r)), 1), f"{what}_MBps_min": round(r[0], 1),
+            f"{what}_MBps_max": round(r[-1], 1)}
+
+
+def host_file_api(nbytes: int, runs: int = 3) -> dict:
     """The path src/cmd.c:90-98 actually calls: snappy_compress(FILE*, size,
     FILE*) and snappy_decompress(FILE*, FILE*) of libsnappy_amd.so, on an
     nbytes text file in /dev/shm (page cache, so the disk is not what is
@@ -309,21 +318,22 @@ def host_file_api(nbytes: int) -> dict:
             libc.fclose(ctypes.c_void_p(fi))
             return rc, t
 
-        best_c = best_d = float("inf")
-        for _ in range(2):  # the first round also allocates the pipeline's pinned slots
+        tcs, tds = [], []
+        for _ in range(1 + runs):  # the first round also allocates the pipeline's pinned slots: untimed
             _, tc = run(lib.snappy_compress, src, snp, size=nbytes)
             assert lib.snappy_amd_last_status() == 0
             rc, td = run(lib.snappy_decompress, snp, dec)
             assert rc == 0 and lib.snappy_amd_last_status() == 0, rc
-            best_c, best_d = min(best_c, tc), min(best_d, td)
+            tcs.append(tc)
+            tds.append(td)
         clen = os.path.getsize(snp.decode())
         ok = os.path.getsize(dec.decode()) == nbytes and \
             np.array_equal(np.fromfile(dec.decode(), dtype=np.uint8), np.fromfile(src.decode(), dtype=np.uint8))
-    return {"bytes": nbytes, "file": "/dev/shm" if d else "tmp", "compressed_bytes": clen,
-            "compress_MBps": round(nbytes / best_c / 1e6, 1), "decompress_MBps": round(nbytes / best_d / 1e6, 1),
-            "round_trip_ok": bool(ok),
-            "note": "snappy_compress / snappy_decompress FILE* entry points (cmd.c's calls), text, best of 2, "
-                    "file I/O + PCIe + kernels"}
+    return dict({"bytes": nbytes, "file": "/dev/shm" if d else "tmp", "compressed_bytes": clen,
+                 "round_trip_ok": bool(ok),
+                 "note": f"snappy_compress / snappy_decompress FILE* entry points (cmd.c's calls), text, median of "
+                         f"{runs} timed runs after one untimed, file I/O + PCIe + kernels"},
+                **rate_stats(nbytes, tcs[1:], "compress"), **rate_stats(nbytes, tds[1:], "decompress"))
 
 
 def config0_file_api(reps: int = 20) -> dict:
@@ -331,7 +341,8 @@ def config0_file_api(reps: int = 20) -> dict:
     (src/cmd.c:90-98's calls) on one 1,000,000-byte text buffer written to a
     file in /dev/shm -- the compiled reference (oracle/_ref/libsnappy_ref.so,
     1 core; CPU-baseline leg only) and libsnappy_amd.so's FILE* path side by
-    side on the same file, in-process through libc stdio, best of `reps`.
+    side on the same file, in-process through libc stdio: the median of the
+    reps - 1 calls after a first untimed one (min / max and the best beside it).
     Both outputs are checked: the two compressed files byte-identical, both
     decodes equal to the input.  MB/s = input bytes / wall second, as
     src/result.c:30-31 prints them."""
@@ -352,7 +363,7 @@ def config0_file_api(reps: int = 20) -> dict:
 
         def time_lib(l, tag):
             snp, dec = (os.path.join(tmp, f"{tag}.{x}").encode() for x in ("snp", "dec"))
-            best_c = best_d = float("inf")
+            tcs, tds = [], []
             for _ in range(reps):
                 for mode in (0, 1):
                     fi = libc.fopen(src if mode == 0 else snp, b"rb")
@@ -366,16 +377,16 @@ def config0_file_api(reps: int = 20) -> dict:
                     libc.fclose(ctypes.c_void_p(fo))
                     t = time.perf_counter() - t0
                     libc.fclose(ctypes.c_void_p(fi))
-                    if mode == 0:
-                        best_c = min(best_c, t)
-                    else:
-                        best_d = min(best_d, t)
+                    (tcs if mode == 0 else tds).append(t)
             comp = open(snp.decode(), "rb").read()
             ok = open(dec.decode(), "rb").read() == a.tobytes()
-            return {"compress_MBps": round(CONFIG0_BYTES / best_c / 1e6, 1),
-                    "decompress_MBps": round(CONFIG0_BYTES / best_d / 1e6, 1),
-                    "round_trip_MBps": round(CONFIG0_BYTES / (best_c + best_d) / 1e6, 1),
-                    "compressed_bytes": len(comp), "round_trip_ok": ok}, comp
+            mc, md = float(np.median(tcs[1:])), float(np.median(tds[1:]))  # (the first call warms up)
+            return dict({"round_trip_MBps": round(CONFIG0_BYTES / (mc + md) / 1e6, 1),
+                         "compressed_bytes": len(comp), "round_trip_ok": ok,
+                         "compress_MBps_best": round(CONFIG0_BYTES / min(tcs) / 1e6, 1),
+                         "decompress_MBps_best": round(CONFIG0_BYTES / min(tds) / 1e6, 1)},
+                        **rate_stats(CONFIG0_BYTES, tcs[1:], "compress"),
+                        **rate_stats(CONFIG0_BYTES, tds[1:], "decompress")), comp
 
         gpu, comp_gpu = time_lib(lib, "gpu")
         assert lib.snappy_amd_last_status() == 0

@@ -64,8 +64,15 @@ int snappy_amd_last_status(void);
 #define SNAPPY_AMD_IDX_MAGIC 0x3158444941504e53ull /* "SNPAIDX1" */
 /* snappy_compress() that also writes the sidecar index of its output to idx */
 int snappy_compress_file_indexed(FILE *file_input, unsigned long long input_size, FILE *file_compressed, FILE *idx);
-/* snappy_decompress() using a sidecar index (SNAPPY_AMD_ERR_INDEX if it does
- * not describe this stream) */
+/* snappy_decompress() using a sidecar index.  SNAPPY_AMD_ERR_INDEX if the
+ * index is not this stream's own block index: a malformed file (magic, count,
+ * an entry outside the stream or decreasing) is refused before any decoding;
+ * an entry moved off an element boundary is refused by the decode (each
+ * block's element chain must end exactly at the next entry), and a decode
+ * that fails for any other reason is checked against the stream's own index
+ * (GPU index pass): a different sidecar -> ERR_INDEX, the same -> the
+ * stream's error, as snappy_decompress reports it.  Success implies the
+ * sidecar was the stream's index and the output is snappy_decompress's. */
 int snappy_decompress_file_indexed(FILE *file_input, FILE *idx, FILE *file_decompressed);
 
 /* ---- varint preamble (src/varint.c) ---------------------------------- */

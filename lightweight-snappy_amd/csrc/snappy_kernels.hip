@@ -740,6 +740,14 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #define SNAPPY_K1R_ASM_BIG 1
 #endif
 #define K1R_CAND32 "s_lshr_b32 %[s0], %[c], 8\n\t"
+// SNAPPY_K1R64_CAND (A/B): 0 = the two tests as shifts and compares of the
+// segment index; 1 = the residency test as one compare against the lowest
+// resident position (seghi carries (seg_hi - 128) * 256); 2 = no tests
+// (measurement only: a candidate outside the ring reads a wrong register)
+#ifndef SNAPPY_K1R64_CAND
+#define SNAPPY_K1R64_CAND 0
+#endif
+#if SNAPPY_K1R64_CAND == 0
 #define K1R_CAND64                                                                                  \
     "s_lshr_b32 %[s0], %[c], 8\n\t"                                                                \
     "s_add_u32 %[s1], %[s0], 128\n\t"                                                              \
@@ -748,6 +756,19 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     "s_and_b32 %[s0], %[s0], 127\n\t"                                                              \
     "s_cmp_eq_u32 %[s0], 127\n\t"                                                                  \
     "s_cbranch_scc1 L%=_x3\n\t"
+#define K1R_SEGHI64(seg_hi) "s"(seg_hi)
+#elif SNAPPY_K1R64_CAND == 1
+#define K1R_CAND64                                                                                  \
+    "s_cmp_lt_u32 %[c], %[seghi]\n\t"                                                              \
+    "s_cbranch_scc1 L%=_x3\n\t"                                                                    \
+    "s_bfe_u32 %[s0], %[c], 0x70008\n\t"                                                           \
+    "s_cmp_eq_u32 %[s0], 127\n\t"                                                                  \
+    "s_cbranch_scc1 L%=_x3\n\t"
+#define K1R_SEGHI64(seg_hi) "s"(((seg_hi) - kRegs) << 8)
+#else
+#define K1R_CAND64 "s_bfe_u32 %[s0], %[c], 0x70008\n\t"
+#define K1R_SEGHI64(seg_hi) "i"(0)
+#endif
 #define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, CAND, SEGHI)                                          \
     do {                                                                                            \
         uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4;                           \
@@ -960,7 +981,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     uint32_t code, fx, cx;
                     uint32_t e32 = ent, et32 = ent_t;
                     if constexpr (BIG)
-                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND64, "s"(seg_hi));
+                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND64, K1R_SEGHI64(seg_hi));
                     else
                         K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND32, "i"(0));
                     ent = (uint16_t)e32;
@@ -2036,6 +2057,12 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
 #ifndef SNAPPY_K4_SPAN_ADAPT
 #define SNAPPY_K4_SPAN_ADAPT 1
 #endif
+#ifndef SNAPPY_K4_JUMP_MAX
+#define SNAPPY_K4_JUMP_MAX 1
+#endif
+#ifndef SNAPPY_K4_PACKED_SCAN
+#define SNAPPY_K4_PACKED_SCAN 1
+#endif
     // the last batch was cut by the 1,024-byte output span (long copies): parse one
     // half only -- more elements would be cut again (repeat-like data)
     bool span_cut = false;
@@ -2085,11 +2112,21 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 const uint32_t lv = k ? b4 & (0xFFFFFFFFu >> ((32 - 8 * k) & 31)) : m;
                 const uint32_t size = t == 0 ? lv + k + 2 : (0x5320u >> (4 * t)) & 0xF;
                 // positions as ds_bpermute addresses (4 x position); one >= 256 has
-                // left the 64: its bpermute result is discarded, so no masking
+                // left the 64 and must stay >= 256 (its exact value is never used).
+                // Every jump goes forward (an element is >= 2 bytes: T[a / 4] > a for
+                // a < 256), so max(bpermute, a) is the jump inside the 64 and keeps an
+                // exited position >= 256 (bpermute wraps addr[7:2]): one v_max per
+                // step instead of a compare and a select
                 const uint32_t J1 = 4 * lane + 4 * (size < 64 ? size : 64);
+#if SNAPPY_K4_JUMP_MAX
+#define JUMP(T, a) ({ const uint32_t _a = (a);                                            \
+        const uint32_t _g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)_a, (int)(T));     \
+        _g > _a ? _g : _a; })
+#else
 #define JUMP(T, a) ({ const uint32_t _a = (a);                                            \
         const uint32_t _g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)_a, (int)(T));     \
         _a < 256 ? _g : _a; })
+#endif
                 const uint32_t J2 = JUMP(J1, J1);
                 const uint32_t J4 = JUMP(J2, J2);
                 const uint32_t J8 = JUMP(J4, J4);
@@ -2167,9 +2204,26 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
         // exclusive prefix sums of compressed sizes and output lengths over
         // the batch (64-bit safe: garbage past E is zeroed)
         const bool live = lane < E;
+#if SNAPPY_K4_PACKED_SCAN
+        // both scans as one over size | len << 16, each clamped to 1,023: exact for
+        // every lane, because only the batch's last element can exceed 440 in either
+        // (an element followed by another of its half is < 64 bytes; one that ends a
+        // half is followed by another half only when that starts <= 440 bytes into
+        // the window), so a clamped value never enters another lane's prefix, and 64
+        // clamped values sum below 2^16 (no carry between the halves)
+        uint32_t in_off, out_off;
+        {
+            const uint32_t pk = live ? (__builtin_elementwise_min(e_size, 1023u) |
+                                        (__builtin_elementwise_min(e_len, 1023u) << 16)) : 0u;
+            const uint32_t ex = wave_incl_scan(pk) - pk;
+            in_off = ex & 0xFFFF;
+            out_off = ex >> 16;
+        }
+#else
         uint32_t tot_in, tot_out;
         const uint32_t in_off = wave_excl_scan(live ? e_size : 0, lane, &tot_in);
         const uint32_t out_off = wave_excl_scan(live ? e_len : 0, lane, &tot_out);
+#endif
         // validity in stream order: stop at the first element that runs past the
         // unit (truncated / overrun), reaches before the stream start, or needs
         // an earlier unit's bytes (pass 1: DEFER); an element running past the

@@ -740,12 +740,16 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #define SNAPPY_K1R_ASM_BIG 1
 #endif
 #define K1R_CAND32 "s_lshr_b32 %[s0], %[c], 8\n\t"
-// SNAPPY_K1R64_CAND (A/B): 0 = the two tests as shifts and compares of the
-// segment index; 1 = the residency test as one compare against the lowest
-// resident position (seghi carries (seg_hi - 128) * 256); 2 = no tests
-// (measurement only: a candidate outside the ring reads a wrong register)
+// SNAPPY_K1R64_CAND (A/B, 1 GiB of 64 KiB text blocks, outputs identical,
+// profiles/r05b_ab_*, r05c_ab_*): 0 = the two tests as shifts and compares of
+// the segment index (18.70 ms); 1 = the residency test as one compare of the
+// candidate against the lowest resident position (seghi carries (seg_hi - 128)
+// * 256) and the segment's register by one s_bfe (18.08-18.16 ms, kept);
+// 2 = no tests (measurement only, wrong output: 17.55 ms, the most the tests
+// can cost); 3 = as 1 with the wrap pair 127 / 0 read branch-free (a
+// scalar-mask select of v2; 18.19-18.23 ms, random 1 % faster)
 #ifndef SNAPPY_K1R64_CAND
-#define SNAPPY_K1R64_CAND 0
+#define SNAPPY_K1R64_CAND 1
 #endif
 #if SNAPPY_K1R64_CAND == 0
 #define K1R_CAND64                                                                                  \
@@ -765,14 +769,29 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     "s_cmp_eq_u32 %[s0], 127\n\t"                                                                  \
     "s_cbranch_scc1 L%=_x3\n\t"
 #define K1R_SEGHI64(seg_hi) "s"(((seg_hi) - kRegs) << 8)
+#elif SNAPPY_K1R64_CAND == 3
+// the residency test as in 1; the wrap pair 127 / 0 without a branch: the
+// second register of the pair is ring register 0 (v2) when the first is 127
+// (the indexed pair read v130 there), selected by a scalar mask
+#define K1R_CAND64                                                                                  \
+    "s_cmp_lt_u32 %[c], %[seghi]\n\t"                                                              \
+    "s_cbranch_scc1 L%=_x3\n\t"                                                                    \
+    "s_bfe_u32 %[s0], %[c], 0x70008\n\t"                                                           \
+    "s_cmp_eq_u32 %[s0], 127\n\t"                                                                  \
+    "s_cselect_b64 %[wm], -1, 0\n\t"
+#define K1R_WRAP64 "v_cndmask_b32_e64 %[t4], %[t4], v2, %[wm]\n\t"
+#define K1R_SEGHI64(seg_hi) "s"(((seg_hi) - kRegs) << 8)
 #else
 #define K1R_CAND64 "s_bfe_u32 %[s0], %[c], 0x70008\n\t"
 #define K1R_SEGHI64(seg_hi) "i"(0)
 #endif
-#define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, CAND, SEGHI)                                          \
+#ifndef K1R_WRAP64
+#define K1R_WRAP64 ""
+#endif
+#define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, CAND, SEGHI, WRAP)                                    \
     do {                                                                                            \
         uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4;                           \
-        uint64_t _valid, _hm;                                                                       \
+        uint64_t _valid, _hm, _wm;                                                                  \
         asm volatile(                                                                               \
             "s_mov_b32 %[m0s], m0\n\t"                                                              \
             "s_cmp_gt_u32 %[skip], %[skipmax]\n\t" /* a step of 2 within DMAX probes: C++ round */   \
@@ -804,6 +823,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "v_mov_b32_e32 %[t3], v2\n\t"                                                           \
             "v_mov_b32_e32 %[t4], v3\n\t"                                                           \
             "s_set_gpr_idx_off\n\t"                                                                 \
+            WRAP                                                                                    \
             "s_bfe_u32 %[s1], %[c], 0x60002\n\t"                                                    \
             "s_lshl_b64 %[hm], -1, %[s1]\n\t" /* lanes >= l0 take register R */                     \
             "s_and_b32 %[s0], %[c], -4\n\t"                                                         \
@@ -912,7 +932,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             : [p] "+s"(p), [skip] "+s"(skip), [lane0] "+s"(lane0), [pend] "+s"(pend), [dka] "+s"(dka), \
               [dkb] "+s"(dkb), [dkn] "+s"(dkn), [code] "=&s"(code), [f] "=&s"(fx), [c] "=&s"(cx),      \
               [m0s] "=&s"(_m0s), [pf] "=&s"(_pf), [s0] "=&s"(_s0), [s1] "=&s"(_s1), [s2] "=&s"(_s2),   \
-              [s3] "=&s"(_s3), [valid] "=&s"(_valid), [hm] "=&s"(_hm), [ent] "+v"(e32),              \
+              [s3] "=&s"(_s3), [valid] "=&s"(_valid), [hm] "=&s"(_hm), [wm] "=&s"(_wm), [ent] "+v"(e32), \
               [entt] "+v"(et32), [tka] "+v"(tka), [tkb] "+v"(tkb), [t0] "=&v"(_t0), [t1] "=&v"(_t1),  \
               [t2] "=&v"(_t2), [t3] "=&v"(_t3), [t4] "=&v"(_t4)                                       \
             : [q0] "s"(q0), [L] "s"(L), [lm16] "s"(L - 16), [mwin] "s"(m_win), [seghi] SEGHI,         \
@@ -981,9 +1001,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     uint32_t code, fx, cx;
                     uint32_t e32 = ent, et32 = ent_t;
                     if constexpr (BIG)
-                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND64, K1R_SEGHI64(seg_hi));
+                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND64, K1R_SEGHI64(seg_hi), K1R_WRAP64);
                     else
-                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND32, "i"(0));
+                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND32, "i"(0), "");
                     ent = (uint16_t)e32;
                     ent_t = (uint8_t)et32;
                     if (code == 1) break;  // skip past the step-1 range, or is_block_end
@@ -1884,9 +1904,9 @@ __device__ __noinline__ int32_t k4_wait(const int32_t *status, uint64_t g_lo, ui
 
 #ifdef SNAPPY_K4_STATS
 #if SNAPPY_TU_DECODE
-__device__ uint64_t g_k4_stats[32768 * 8];
+__device__ uint64_t g_k4_stats[32768 * 16];
 #else
-static __device__ uint64_t g_k4_stats[8];  // (k4_body is parsed, never instantiated, here)
+static __device__ uint64_t g_k4_stats[16];  // (k4_body is parsed, never instantiated, here)
 #endif
 #define K4STAMP(var)                                                                        \
     do {                                                                                    \
@@ -2053,6 +2073,11 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     const uint64_t t_loop = clock64();
     uint32_t n_el = 0, n_batch = 0, n_pass = 0, n_sub = 0, n_far = 0;
     uint64_t sg0 = 0, sg1 = 0, sg2 = 0, ta, tb, tc, td;
+    // batch shape: halves parsed, parsed elements (E), and what ended the batch
+    // before E: a bad element (tail / error), a literal leaving the window, the
+    // output span; batches with E == 64; batches after a span cut (one half)
+    uint32_t n_half = 0, n_E = 0, n_cut_bad = 0, n_cut_long = 0, n_cut_span = 0, n_full = 0, n_spanb = 0;
+    uint32_t n_stop_win = 0;  // batches whose halves stopped at the window limit (E < 64)
 #endif
 #ifndef SNAPPY_K4_SPAN_ADAPT
 #define SNAPPY_K4_SPAN_ADAPT 1
@@ -2165,9 +2190,19 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
 #define SNAPPY_K4_HALVES 3
 #endif
             uint32_t hpos = o + xa;
+#ifdef SNAPPY_K4_STATS
+            n_half++;
+            n_spanb += span_cut;
+#endif
 #pragma unroll
             for (int hh = 1; hh < SNAPPY_K4_HALVES; hh++) {
+#ifdef SNAPPY_K4_STATS
+                n_stop_win += (E < 64 && hpos > 440 && !span_cut) ? 1u : 0u;
+#endif
                 if (!(E < 64 && hpos <= 440) || (SNAPPY_K4_SPAN_ADAPT && span_cut)) break;
+#ifdef SNAPPY_K4_STATS
+                n_half++;
+#endif
                 uint32_t bx0, bb4, eb, xb;
                 parse_half(hpos, bx0, bb4, eb, xb);
                 const int sa = (int)(4 * (lane - E));
@@ -2259,6 +2294,11 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
         }
         const uint64_t badm = __ballot(live && e_err != SNAPPY_ST_OK);
         uint32_t nexec = E;
+#ifdef SNAPPY_K4_STATS
+        n_E += E;
+        n_full += E == 64;
+        const uint32_t nexec_e = E;
+#endif
         if (badm) {
             nexec = (uint32_t)__builtin_ctzll(badm);
             int32_t er = __builtin_amdgcn_readlane(e_err, nexec);
@@ -2312,8 +2352,16 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             // and 2048 + kK4MapBits <= ring - 64
             static_assert(2048 + kK4MapBits <= kK4Ring - 64, "K4: the ring must hold [F, op_end)");
             const uint64_t over = __ballot(lane < nexec && lane > 0 && out_off + e_len > kK4MapBits);
+#ifdef SNAPPY_K4_STATS
+            const uint32_t nexec_l = nexec;
+#endif
             if (over) nexec = (uint32_t)__builtin_ctzll(over);
             span_cut = over != 0;
+#ifdef SNAPPY_K4_STATS
+            n_cut_span += nexec < nexec_l;
+            n_cut_long += (longm != 0) && nexec_l < E;
+            n_cut_bad += (badm != 0) && (uint32_t)__builtin_ctzll(badm) < nexec_e;
+#endif
             if constexpr (BACK) {
                 // copies reading earlier units: wait until those bytes are in HBM
                 uint64_t bm = __ballot(e_back && lane < nexec);
@@ -2481,7 +2529,15 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     if (st == SNAPPY_ST_OK && allow_back && !skip1 && base + unit < n && ip != clen) st = SNAPPY_ST_INDEX;
 #ifdef SNAPPY_K4_STATS
     if (lane == 0 && u < 32768) {
-        uint64_t *g = g_k4_stats + 8 * u;
+        uint64_t *g = g_k4_stats + 16 * u;
+        g[8] = n_half;
+        g[9] = n_E;
+        g[10] = n_cut_bad;
+        g[11] = n_cut_long;
+        g[12] = n_cut_span;
+        g[13] = n_full;
+        g[14] = n_spanb;
+        g[15] = n_stop_win;
         g[0] = clock64() - t_loop;
         g[1] = n_el | ((uint64_t)n_far << 32);
         g[2] = n_batch;

@@ -15,14 +15,14 @@ comp, offs = c.compress_tensor(x, chunk=chunk, layout=snappy_amd.STREAMS)
 back = c.decompress_tensor(comp, offs, n, chunk=chunk, layout=snappy_amd.STREAMS)
 assert torch.equal(back, x)
 units = n // chunk
-buf = np.zeros(units * 8, dtype=np.uint64)
+buf = np.zeros(units * 16, dtype=np.uint64)
 lib = snappy_amd.lib()
 lib.snappy_amd_debug_k4_stats.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
-assert lib.snappy_amd_debug_k4_stats(buf.ctypes.data_as(ctypes.c_void_p), units * 8) == 0
-st = buf.reshape(units, 8)
+assert lib.snappy_amd_debug_k4_stats(buf.ctypes.data_as(ctypes.c_void_p), units * 16) == 0
+st = buf.reshape(units, 16)
 far = (st[:, 1] >> 32).astype(np.float64)
 st = st.astype(np.float64)
-st[:, 1] = (buf.reshape(units, 8)[:, 1] & 0xFFFFFFFF).astype(np.float64)
+st[:, 1] = (buf.reshape(units, 16)[:, 1] & 0xFFFFFFFF).astype(np.float64)
 m = st.mean(axis=0)
 print(f"{kind} units {units}: elements/unit {m[1]:.0f} batches {m[2]:.0f} passes {m[3]:.0f} pass steps {m[4]:.0f} (passes + pointer-jump steps)"
       f" passes reading HBM (copies beyond the ring) {far.mean():.0f}")
@@ -30,3 +30,8 @@ print(f"cycles/unit {m[0]:.0f}  cycles/element {m[0]/m[1]:.1f}  cycles/batch {m[
 for i, nm in ((5, "window+candidate parse"), (6, "doubling+gather+scans+validate"), (7, "execute (passes)")):
     print(f"  {nm:32s} {m[i]/m[2]:7.0f} cycles/batch  {100*m[i]/m[0]:5.1f}%")
 print(f"  per pass {m[7]/max(m[3],1):.0f} cycles")
+b = max(m[2], 1)
+print(f"batch shape: halves/batch {m[8]/b:.2f}  parsed elements/batch {m[9]/b:.1f}  executed {m[1]/b:.1f}  "
+      f"E == 64 {100*m[13]/b:.1f}%  halves stopped at the window {100*m[15]/b:.1f}%  after a span cut {100*m[14]/b:.1f}%")
+print(f"cut before E by: a bad/tail element {100*m[10]/b:.1f}%  a literal leaving the window {100*m[11]/b:.1f}%  "
+      f"the output span {100*m[12]/b:.1f}%")

@@ -601,6 +601,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     uint32_t adr = 0, word = 0;               // the lane's table record address and its insert word
     uint32_t pdnz = 0;
     uint64_t m_win = 0, m_win17 = 0;
+    uint64_t m_pdz = 0;  // lanes whose in-window predecessor carries the same tag (pdnz == 0)
     bool lsw = false;  // the lane-space data describe the current window
 #define WINDOW_AT(qq)                                                                              \
     do {                                                                                           \
@@ -629,12 +630,18 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         pdc = q0 + lane - _pd;                                                                     \
         const uint32_t _hp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - _pd) << 2), (int)hv); \
         pdnz = _hp == hv ? 0u : 1u; /* 0 iff the predecessor's tag matches */                     \
+        if (SNAPPY_K1R_ASM_V4) m_pdz = __ballot(_hp == hv);                                        \
         /* probe lanes: <= 62 and not past is_block_end (L - p >= 16, 17 at skip 64) */           \
         const int32_t _w16 = (int32_t)(L - 16 - q0), _w17 = (int32_t)(L - 17 - q0);              \
-        m_win = __ballot((int32_t)lane <= _w16 && lane <= 62);                                     \
+        const bool _inw = (int32_t)lane <= _w16 && lane <= 62;                                     \
+        m_win = __ballot(_inw);                                                                    \
         m_win17 = __ballot((int32_t)lane <= _w17 && lane <= 62);                                   \
         adr = TBL_ADR(hv & 0xFFFF);                                                                \
         word = (q0 + lane) | (hv & 0xFF0000u);                                                     \
+        if (SNAPPY_K1R_ASM_V6 && !_inw) { /* the asm hit test sees the window mask in the lane data */ \
+            word |= 1u << 24;                                                                      \
+            pdnz = 1;                                                                              \
+        }                                                                                          \
         lsw = true; /* the caller reads ent */                                                     \
     } while (0)
 
@@ -788,6 +795,270 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #ifndef K1R_WRAP64
 #define K1R_WRAP64 ""
 #endif
+// SNAPPY_K1R_ASM_V2 (A/B): the hit path with fewer scalar instructions on the
+// round's dependency chain: the hit branch on the SCC of the s_and that makes
+// the hit mask; the candidate used unmasked (it is < 65,536: a u16 table entry
+// or a position) and the gather addresses without clearing their low bits
+// (ds_bpermute reads addr[7:2], and adding 4 x lane never carries out of bits
+// 0-1); the first differing dword found by one s_ff1 of vcc_lo (> 15 or -1 =
+// 64 equal bytes); the next lane0 as f + length; one signed compare against
+// lim0 = min(62 - RMIN, L - 16 - q0) for "continue", the exit decided after it
+#ifndef SNAPPY_K1R_ASM_V2
+#define SNAPPY_K1R_ASM_V2 1
+#endif
+// SNAPPY_K1R_ASM_V3 (with V2): the prefix length with fewer VALU before its
+// v_readlane: (clz(xor) | 32 x lane) read back, divided by 8 in SALU (lanes
+// with equal dwords are never read, so no `| 1` guard on the clz)
+#ifndef SNAPPY_K1R_ASM_V3
+#define SNAPPY_K1R_ASM_V3 1
+#endif
+// SNAPPY_K1R_ASM_V4: the hit mask in SALU from two lane masks -- the table
+// lanes' tag hits (one SDWA compare to an SGPR pair) and pdz, the lanes whose
+// in-window predecessor's tag matches (per window) -- instead of a VALU select
+// of the two tag differences and a compare
+#ifndef SNAPPY_K1R_ASM_V4
+#define SNAPPY_K1R_ASM_V4 0
+#endif
+#if SNAPPY_K1R_ASM_V4
+#define K1R_V4_HIT                                                                                  \
+    "v_cmp_eq_u32_sdwa %[hm], %[entt], %[word] src0_sel:DWORD src1_sel:WORD_1\n\t"                   \
+    "v_cndmask_b32_sdwa %[t1], %[pdc], %[ent], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "             \
+    "src0_sel:DWORD src1_sel:WORD_0\n\t" /* the candidate of every lane */                          \
+    "s_andn2_b64 %[wm], %[pdz], vcc\n\t"                                                            \
+    "s_and_b64 %[hm], %[hm], vcc\n\t"                                                               \
+    "s_or_b64 %[hm], %[hm], %[wm]\n\t"
+#else
+#define K1R_V4_HIT                                                                                  \
+    "v_xor_b32_sdwa %[t0], %[entt], %[word] dst_sel:DWORD dst_unused:UNUSED_PAD "                    \
+    "src0_sel:DWORD src1_sel:WORD_1\n\t"                                                            \
+    "v_cndmask_b32_sdwa %[t1], %[pdc], %[ent], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "             \
+    "src0_sel:DWORD src1_sel:WORD_0\n\t" /* the candidate of every lane */                          \
+    "v_cndmask_b32_sdwa %[t0], %[pdnz], %[t0], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "             \
+    "src0_sel:DWORD src1_sel:" K1R_V6_T0SEL "\n\t"                                                   \
+    "v_cmp_eq_u32_e64 %[hm], 0, %[t0]\n\t"
+#endif
+// SNAPPY_K1R_ASM_V5 (with V2/V3): three scalar instructions fewer per hit round:
+// the candidate pair's lane select by a VALU compare into vcc (free between the
+// round's two uses of it) instead of a 64-bit shifted mask; lo0 = lane0 - (lane0
+// < f) by s_subb on the compare's SCC; dkn not cleared after the drain (the hit
+// round sets it to 1 before the loop goes on; the C++ finish of codes 4 and 5
+// sets it itself)
+#ifndef SNAPPY_K1R_ASM_V5
+#define SNAPPY_K1R_ASM_V5 1
+#endif
+#if SNAPPY_K1R_ASM_V5
+#define K1R_V5_ROT "v_cmp_le_u32_e32 vcc, %[s1], %[lane]\n\t" /* lanes >= l0 take register R */
+#define K1R_V5_SEL "v_cndmask_b32_e32 %[t3], %[t4], %[t3], vcc\n\t"
+#define K1R_V5_LO0                                                                                  \
+    "s_cmp_lt_u32 %[lane0], %[f]\n\t"                                                               \
+    "s_subb_u32 %[s0], %[lane0], 0\n\t" /* lo0 */
+#else
+#define K1R_V5_ROT "s_lshl_b64 %[hm], -1, %[s1]\n\t" /* lanes >= l0 take register R */
+#define K1R_V5_SEL "v_cndmask_b32_e64 %[t3], %[t4], %[t3], %[hm]\n\t"
+#define K1R_V5_LO0                                                                                  \
+    "s_mov_b32 %[dkn], 0\n\t"                                                                       \
+    "s_add_i32 %[s0], %[lane0], -1\n\t"                                                             \
+    "s_cmp_lt_u32 %[lane0], %[f]\n\t"                                                               \
+    "s_cselect_b32 %[s0], %[s0], %[lane0]\n\t" /* lo0 */
+#endif
+// SNAPPY_K1R_ASM_V6 (with V2/V3/V5): five more scalar instructions off the hit
+// round: the window mask folded into the per-window lane data (a lane past the
+// window gets bit 24 of its insert word -- its tag compare then differs in bit
+// 8 -- and a non-zero pdnz), so only the miss path still ands it into `valid`;
+// the dwords at pf gathered from (pf - 1) / 4 and funnelled by v_alignbit with
+// the scalar shift -8 pf (bits 4:0 = 32 - 8 (pf % 4), and 0 takes the next
+// dword: the one at pf when pf % 4 == 0), one s_mul instead of an and, a
+// multiply and an add for a perm selector; the clamp of the match length to
+// the block end only on the exit path (the continue test lane0 <= lim0 already
+// implies pf + len <= L - 16)
+#ifndef SNAPPY_K1R_ASM_V6
+#define SNAPPY_K1R_ASM_V6 1
+#endif
+#if SNAPPY_K1R_ASM_V6
+#define K1R_V6_MWIN_HIT ""
+#define K1R_V6_MWIN_NOHIT "s_and_b64 %[valid], %[valid], %[mwin]\n\t"
+#define K1R_V6_T0SEL "WORD_0"
+#define K1R_V6_SEL2A "s_mul_i32 %[s2], %[pf], -8\n\t"
+#define K1R_V6_SEL2B ""
+#define K1R_V6_FUNNEL_PA "v_alignbit_b32 %[t2], %[t2], %[t1], %[s2]\n\t"
+#define K1R_V6_DRAIN                                                                                \
+    "s_mov_b32 m0, %[pend]\n\t" /* (gfx950 refuses two SGPRs in a v_writelane: m0 stays) */          \
+    "v_writelane_b32 %[tka], %[dka], m0\n\t"                                                        \
+    "v_writelane_b32 %[tkb], %[dkb], m0\n\t"
+#else
+#define K1R_V6_MWIN_HIT "s_and_b64 %[valid], %[valid], %[mwin]\n\t"
+#define K1R_V6_MWIN_NOHIT ""
+#define K1R_V6_T0SEL "BYTE_0"
+#define K1R_V6_SEL2A "s_and_b32 %[s2], %[pf], 3\n\ts_mul_i32 %[s2], %[s2], 0xfefefeff\n\t"
+#define K1R_V6_SEL2B "s_add_i32 %[s2], %[s2], 0x7060504\n\t"
+#define K1R_V6_FUNNEL_PA "v_perm_b32 %[t2], %[t2], %[t1], %[s2]\n\t"
+#define K1R_V6_DRAIN                                                                                \
+    "s_mov_b32 m0, %[pend]\n\t"                                                                     \
+    "v_writelane_b32 %[tka], %[dka], m0\n\t"                                                        \
+    "v_writelane_b32 %[tkb], %[dkb], m0\n\t"
+#endif
+#if SNAPPY_K1R_ASM_V2 && SNAPPY_K1R_ASM_V3
+#define K1R_V3_LEN                                                                                  \
+    "v_xor_b32_e32 %[t2], %[t2], %[t3]\n\t"                                                         \
+    "v_ffbh_u32_e32 %[t2], %[t2]\n\t"                                                               \
+    "v_lshl_or_b32 %[t2], %[lane4], 3, %[t2]\n\t" /* 8 x the prefix length if this dword differs */
+#define K1R_V3_DIV "s_lshr_b32 %[s0], %[s0], 3\n\t"
+#else
+#define K1R_V3_LEN                                                                                  \
+    "v_xor_b32_e32 %[t2], %[t2], %[t3]\n\t"                                                         \
+    "v_or_b32_e32 %[t2], 1, %[t2]\n\t"                                                              \
+    "v_ffbh_u32_e32 %[t2], %[t2]\n\t"                                                               \
+    "v_lshrrev_b32_e32 %[t2], 3, %[t2]\n\t"                                                         \
+    "v_or_b32_e32 %[t2], %[t2], %[lane4]\n\t" /* the prefix length if this dword differs */
+#define K1R_V3_DIV ""
+#endif
+// SNAPPY_K1R_ASM_V7 (with V6): p (read only after the loop) is set on the exit
+// path alone, and the prefix length comes back from v_readlane finished
+// ((clz >> 3) | 4 x lane by v_bfe + v_lshl_or) instead of a scalar division
+#ifndef SNAPPY_K1R_ASM_V7
+#define SNAPPY_K1R_ASM_V7 1
+#endif
+// SNAPPY_K1R_ASM_V8 (with V6): skip is not reset by a hit round.  Everywhere,
+// dkn == 1 (a match's token pending) comes with skip == 32 (the C++ code sets
+// both together), so the loop keeps skip stale after a hit and the miss path
+// and the loop's exit take 32 whenever dkn is 1
+#ifndef SNAPPY_K1R_ASM_V8
+#define SNAPPY_K1R_ASM_V8 1
+#endif
+#if SNAPPY_K1R_ASM_V8
+#define K1R_V8_SKIP ""
+#define K1R_V8_SKIPFIX "s_cmp_eq_u32 %[dkn], 0\n\ts_cselect_b32 %[skip], %[skip], 32\n\t"
+#else
+#define K1R_V8_SKIP "s_mov_b32 %[skip], 32\n\t"
+#define K1R_V8_SKIPFIX ""
+#endif
+// SNAPPY_K1R_ASM_V9 (with V8): the deferred token's first word by one
+// s_pack_ll_b32_b16 (pf and the length are < 2^16); the miss path does not
+// clear dka / dkb (with dkn = 0 the next drain writes lane pend, which the
+// next token overwrites) and steps lane0 first, p = q0 + lane0 from it
+#ifndef SNAPPY_K1R_ASM_V9
+#define SNAPPY_K1R_ASM_V9 1
+#endif
+#if SNAPPY_K1R_ASM_V9
+#define K1R_V9_DKA "s_pack_ll_b32_b16 %[dka], %[pf], %[s0]\n\t"
+#define K1R_V9_DKZERO ""
+#define K1R_V9_NOHIT_P                                                                              \
+    "s_add_u32 %[lane0], %[s1], %[s0]\n\t" /* lane0 - 1 + nk + the step-2 probe */                 \
+    "s_add_u32 %[lane0], %[lane0], %[s3]\n\t"                                                       \
+    "s_add_u32 %[p], %[q0], %[lane0]\n\t"
+#define K1R_V9_NOHIT_L0 ""
+#else
+#define K1R_V9_DKA "s_lshl_b32 %[s1], %[s0], 16\n\ts_or_b32 %[dka], %[s1], %[pf]\n\t"
+#define K1R_V9_DKZERO "s_mov_b32 %[dka], 0\n\ts_mov_b32 %[dkb], 0\n\t"
+#define K1R_V9_NOHIT_P                                                                              \
+    "s_add_u32 %[p], %[q0], %[lane0]\n\t"                                                           \
+    "s_add_u32 %[p], %[p], %[s0]\n\t"                                                               \
+    "s_add_u32 %[p], %[p], %[s3]\n\t"                                                               \
+    "s_add_i32 %[p], %[p], -1\n\t"
+#define K1R_V9_NOHIT_L0 "s_sub_u32 %[lane0], %[p], %[q0]\n\t"
+#endif
+#if SNAPPY_K1R_ASM_V7
+#define K1R_V7_P ""
+#undef K1R_V3_LEN
+#undef K1R_V3_DIV
+#define K1R_V3_LEN                                                                                  \
+    "v_xor_b32_e32 %[t2], %[t2], %[t3]\n\t"                                                         \
+    "v_ffbh_u32_e32 %[t2], %[t2]\n\t"                                                               \
+    "v_bfe_u32 %[t2], %[t2], 3, 2\n\t"                                                              \
+    "v_lshl_or_b32 %[t2], %[lane], 2, %[t2]\n\t" /* the prefix length if this dword differs */
+#define K1R_V3_DIV ""
+#else
+#define K1R_V7_P "s_add_u32 %[p], %[pf], %[s0]\n\t"
+#endif
+#if SNAPPY_K1R_ASM_V2 && SNAPPY_K1R_ASM_V6
+#define K1R_V2_TAIL                                                                                 \
+    "s_ff1_i32_b32 %[s1], vcc_lo\n\t"                                                               \
+    "s_cmp_gt_u32 %[s1], 15\n\t"                                                                    \
+    "s_cbranch_scc1 L%=_x4\n\t"                                                                     \
+    "v_readlane_b32 %[s0], %[t2], %[s1]\n\t"                                                        \
+    K1R_V3_DIV                                                                                      \
+    "s_cmp_lt_u32 %[s0], 4\n\t" /* (pf <= L - 16: the clamp below never makes it < 4) */            \
+    "s_cbranch_scc1 L%=_x5\n\t"                                                                     \
+    "s_add_u32 %[lane0], %[f], %[s0]\n\t"                                                           \
+    K1R_V7_P                                                                                        \
+    K1R_V9_DKA                                                                                      \
+    "s_sub_u32 %[dkb], %[pf], %[c]\n\t"                                                             \
+    "s_mov_b32 %[dkn], 1\n\t"                                                                       \
+    K1R_V8_SKIP                                                                                     \
+    "s_cmp_le_i32 %[lane0], %[lim0]\n\t" /* implies pf + len <= L - 16: no clamp */                 \
+    "s_cbranch_scc1 L%=_top\n\t"                                                                    \
+    "s_sub_u32 %[s2], %[L], %[pf]\n\t" /* leaving: the length clamped to the block end */         \
+    "s_min_u32 %[s0], %[s0], %[s2]\n\t"                                                             \
+    "s_add_u32 %[p], %[pf], %[s0]\n\t"                                                              \
+    "s_sub_u32 %[lane0], %[p], %[q0]\n\t"                                                           \
+    "s_lshl_b32 %[s1], %[s0], 16\n\t"                                                               \
+    "s_or_b32 %[dka], %[s1], %[pf]\n\t"                                                             \
+    "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                                \
+    "s_cbranch_scc1 L%=_x1\n\t"                                                                     \
+    "s_branch L%=_x2\n"
+#endif
+#if SNAPPY_K1R_ASM_V2
+#define K1R_V2_HITBR "s_cbranch_scc0 L%=_nohit\n\t" /* SCC = (hm != 0) */
+#if SNAPPY_K1R_ASM_V6
+#define K1R_V2_PA "v_add3_u32 %[t2], %[pf], -1, %[lane4]\n\t" /* dwords from (pf - 1) / 4: see V6 */
+#else
+#define K1R_V2_PA "v_add_u32_e32 %[t2], %[pf], %[lane4]\n\t"
+#endif
+#define K1R_V2_CMASK ""
+#define K1R_V2_CA "v_add_u32_e32 %[t1], %[c], %[lane4]\n\t"
+#ifndef K1R_V2_TAIL
+#define K1R_V2_TAIL                                                                                 \
+    "s_sub_u32 %[s2], %[L], %[pf]\n\t"                                                              \
+    "s_ff1_i32_b32 %[s1], vcc_lo\n\t"                                                               \
+    "s_cmp_gt_u32 %[s1], 15\n\t"                                                                    \
+    "s_cbranch_scc1 L%=_x4\n\t"                                                                     \
+    "v_readlane_b32 %[s0], %[t2], %[s1]\n\t"                                                        \
+    K1R_V3_DIV                                                                                      \
+    "s_min_u32 %[s0], %[s0], %[s2]\n\t"                                                             \
+    "s_cmp_lt_u32 %[s0], 4\n\t"                                                                     \
+    "s_cbranch_scc1 L%=_x5\n\t"                                                                     \
+    "s_add_u32 %[lane0], %[f], %[s0]\n\t"                                                           \
+    "s_add_u32 %[p], %[pf], %[s0]\n\t"                                                              \
+    "s_lshl_b32 %[s1], %[s0], 16\n\t"                                                               \
+    "s_or_b32 %[dka], %[s1], %[pf]\n\t"                                                             \
+    "s_sub_u32 %[dkb], %[pf], %[c]\n\t"                                                             \
+    "s_mov_b32 %[dkn], 1\n\t"                                                                       \
+    "s_mov_b32 %[skip], 32\n\t"                                                                     \
+    "s_cmp_le_i32 %[lane0], %[lim0]\n\t"                                                            \
+    "s_cbranch_scc1 L%=_top\n\t"                                                                    \
+    "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                                \
+    "s_cbranch_scc1 L%=_x1\n\t"                                                                     \
+    "s_branch L%=_x2\n"
+#endif
+#else
+#define K1R_V2_HITBR "s_cmp_eq_u64 %[hm], 0\n\ts_cbranch_scc1 L%=_nohit\n\t"
+#define K1R_V2_PA "s_and_b32 %[s0], %[pf], -4\n\tv_add_u32_e32 %[t2], %[s0], %[lane4]\n\t"
+#define K1R_V2_CMASK "s_and_b32 %[c], %[c], 0xffff\n\t"
+#define K1R_V2_CA "s_and_b32 %[s0], %[c], -4\n\tv_add_u32_e32 %[t1], %[s0], %[lane4]\n\t"
+#define K1R_V2_TAIL                                                                                 \
+    "s_and_b32 %[s1], vcc_lo, 0xffff\n\t"                                                           \
+    "s_cmp_eq_u32 %[s1], 0\n\t"                                                                     \
+    "s_cbranch_scc1 L%=_x4\n\t"                                                                     \
+    "s_ff1_i32_b32 %[s1], %[s1]\n\t"                                                                \
+    "s_nop 1\n\t"                                                                                   \
+    "v_readlane_b32 %[s0], %[t2], %[s1]\n\t"                                                        \
+    "s_sub_u32 %[s1], %[L], %[pf]\n\t"                                                              \
+    "s_min_u32 %[s0], %[s0], %[s1]\n\t"                                                             \
+    "s_cmp_lt_u32 %[s0], 4\n\t"                                                                     \
+    "s_cbranch_scc1 L%=_x5\n\t"                                                                     \
+    "s_add_u32 %[p], %[pf], %[s0]\n\t"                                                              \
+    "s_sub_u32 %[lane0], %[p], %[q0]\n\t"                                                           \
+    "s_lshl_b32 %[s1], %[s0], 16\n\t"                                                               \
+    "s_or_b32 %[dka], %[s1], %[pf]\n\t"                                                             \
+    "s_sub_u32 %[dkb], %[pf], %[c]\n\t"                                                             \
+    "s_mov_b32 %[dkn], 1\n\t"                                                                       \
+    "s_mov_b32 %[skip], 32\n\t"                                                                     \
+    "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                                \
+    "s_cbranch_scc1 L%=_x1\n\t"                                                                     \
+    "s_cmp_le_u32 %[lane0], %[l0max]\n\t"                                                           \
+    "s_cbranch_scc1 L%=_top\n\t"                                                                    \
+    "s_branch L%=_x2\n"
+#endif
 #define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, CAND, SEGHI, WRAP)                                    \
     do {                                                                                            \
         uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4;                           \
@@ -799,25 +1070,17 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "L%=_top:\n\t"                                                                          \
             "s_lshl_b64 %[valid], %[dmask], %[lane0]\n\t"                                           \
             "v_cmp_gt_i32_e32 vcc, %[lane0], %[pdl1]\n\t" /* vcc = not in-round */                  \
-            "s_and_b64 %[valid], %[valid], %[mwin]\n\t"                                             \
+            K1R_V6_MWIN_HIT                                                                         \
             "s_waitcnt lgkmcnt(0)\n\t"                                                              \
-            "v_xor_b32_sdwa %[t0], %[entt], %[word] dst_sel:DWORD dst_unused:UNUSED_PAD "            \
-            "src0_sel:DWORD src1_sel:WORD_1\n\t"                                                    \
-            "v_cndmask_b32_sdwa %[t1], %[pdc], %[ent], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "     \
-            "src0_sel:DWORD src1_sel:WORD_0\n\t" /* the candidate of every lane */                  \
-            "v_cndmask_b32_sdwa %[t0], %[pdnz], %[t0], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "     \
-            "src0_sel:DWORD src1_sel:BYTE_0\n\t"                                                    \
-            "v_cmp_eq_u32_e64 %[hm], 0, %[t0]\n\t"                                                  \
+            K1R_V4_HIT                                                                              \
             "s_and_b64 %[hm], %[hm], %[valid]\n\t"                                                  \
-            "s_cmp_eq_u64 %[hm], 0\n\t"                                                             \
-            "s_cbranch_scc1 L%=_nohit\n\t"                                                          \
+            K1R_V2_HITBR                                                                            \
             "s_ff1_i32_b64 %[f], %[hm]\n\t"                                                         \
             "v_readlane_b32 %[c], %[t1], %[f]\n\t"                                                  \
             "s_add_u32 %[pf], %[q0], %[f]\n\t"                                                      \
-            "s_and_b32 %[s0], %[pf], -4\n\t"                                                        \
-            "v_add_u32_e32 %[t2], %[s0], %[lane4]\n\t"                                              \
+            K1R_V2_PA                                                                               \
             "ds_bpermute_b32 %[t2], %[t2], %[dv]\n\t" /* pa: dwords at pf */                        \
-            "s_and_b32 %[c], %[c], 0xffff\n\t"                                                      \
+            K1R_V2_CMASK                                                                            \
             CAND                                                                                    \
             "s_set_gpr_idx_on %[s0], gpr_idx(SRC0)\n\t"                                             \
             "v_mov_b32_e32 %[t3], v2\n\t"                                                           \
@@ -825,76 +1088,43 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "s_set_gpr_idx_off\n\t"                                                                 \
             WRAP                                                                                    \
             "s_bfe_u32 %[s1], %[c], 0x60002\n\t"                                                    \
-            "s_lshl_b64 %[hm], -1, %[s1]\n\t" /* lanes >= l0 take register R */                     \
-            "s_and_b32 %[s0], %[c], -4\n\t"                                                         \
-            "v_add_u32_e32 %[t1], %[s0], %[lane4]\n\t"                                              \
-            "v_cndmask_b32_e64 %[t3], %[t4], %[t3], %[hm]\n\t"                                      \
+            K1R_V5_ROT                                                                              \
+            K1R_V2_CA                                                                               \
+            K1R_V5_SEL                                                                              \
             "ds_bpermute_b32 %[t3], %[t1], %[t3]\n\t" /* ca: dwords at c */                         \
-            "s_mov_b32 m0, %[pend]\n\t" /* the previous round's token, during the gathers */        \
-            "v_writelane_b32 %[tka], %[dka], m0\n\t"                                                \
-            "v_writelane_b32 %[tkb], %[dkb], m0\n\t"                                                \
+            K1R_V6_DRAIN /* the previous round's token, during the gathers */                      \
             "s_add_u32 %[pend], %[pend], %[dkn]\n\t"                                                \
-            "s_mov_b32 %[dkn], 0\n\t"                                                               \
-            "s_add_i32 %[s0], %[lane0], -1\n\t"                                                     \
-            "s_cmp_lt_u32 %[lane0], %[f]\n\t"                                                       \
-            "s_cselect_b32 %[s0], %[s0], %[lane0]\n\t" /* lo0 */                                    \
+            K1R_V5_LO0                                                                              \
             "v_subrev_u32_e32 %[t4], %[s0], %[lane]\n\t"                                            \
             "s_sub_u32 %[s0], %[f], %[s0]\n\t"                                                      \
             "v_cmp_ge_u32_e32 vcc, %[s0], %[t4]\n\t" /* lanes lo0 .. f insert */                    \
-            "s_and_b32 %[s2], %[pf], 3\n\t"                                                         \
-            "s_mul_i32 %[s2], %[s2], 0xfefefeff\n\t"                                                \
+            K1R_V6_SEL2A                                                                            \
             "v_cndmask_b32_e32 %[t4], %[dummy], %[adr], vcc\n\t"                                    \
             "ds_write_b16 %[t4], %[word]\n\t"                                                       \
             "v_lshrrev_b32_e32 %[t4], 1, %[t4]\n\t"                                                 \
             "ds_write_b8_d16_hi %[t4], %[word] offset:%[tagb]\n\t"                                  \
             "ds_read_u16 %[ent], %[adr]\n\t"                                                        \
             "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"                                        \
-            "s_add_i32 %[s2], %[s2], 0x7060504\n\t"                                                 \
+            K1R_V6_SEL2B                                                                            \
             "s_and_b32 %[s3], %[c], 3\n\t"                                                          \
             "s_mul_i32 %[s3], %[s3], 0xfefefeff\n\t"                                                \
             "s_add_i32 %[s3], %[s3], 0x7060504\n\t"                                                 \
             "s_waitcnt lgkmcnt(2)\n\t" /* pa, ca and the inserts; the entry reads stay in flight */ \
             "v_mov_b32_dpp %[t1], %[t2] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
             "v_mov_b32_dpp %[t4], %[t3] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
-            "v_perm_b32 %[t2], %[t2], %[t1], %[s2]\n\t"                                             \
+            K1R_V6_FUNNEL_PA                                                                        \
             "v_perm_b32 %[t3], %[t3], %[t4], %[s3]\n\t"                                             \
             "v_cmp_ne_u32_e32 vcc, %[t2], %[t3]\n\t"                                                \
-            "v_xor_b32_e32 %[t2], %[t2], %[t3]\n\t"                                                 \
-            "v_or_b32_e32 %[t2], 1, %[t2]\n\t"                                                      \
-            "v_ffbh_u32_e32 %[t2], %[t2]\n\t"                                                       \
-            "v_lshrrev_b32_e32 %[t2], 3, %[t2]\n\t"                                                 \
-            "v_or_b32_e32 %[t2], %[t2], %[lane4]\n\t" /* the prefix length if this dword differs */ \
-            "s_and_b32 %[s1], vcc_lo, 0xffff\n\t"                                                   \
-            "s_cmp_eq_u32 %[s1], 0\n\t"                                                             \
-            "s_cbranch_scc1 L%=_x4\n\t"                                                             \
-            "s_ff1_i32_b32 %[s1], %[s1]\n\t"                                                        \
-            "s_nop 1\n\t"                                                                           \
-            "v_readlane_b32 %[s0], %[t2], %[s1]\n\t"                                                \
-            "s_sub_u32 %[s1], %[L], %[pf]\n\t"                                                      \
-            "s_min_u32 %[s0], %[s0], %[s1]\n\t"                                                     \
-            "s_cmp_lt_u32 %[s0], 4\n\t"                                                             \
-            "s_cbranch_scc1 L%=_x5\n\t"                                                             \
-            "s_add_u32 %[p], %[pf], %[s0]\n\t"                                                      \
-            "s_sub_u32 %[lane0], %[p], %[q0]\n\t"                                                   \
-            "s_lshl_b32 %[s1], %[s0], 16\n\t"                                                       \
-            "s_or_b32 %[dka], %[s1], %[pf]\n\t"                                                     \
-            "s_sub_u32 %[dkb], %[pf], %[c]\n\t"                                                     \
-            "s_mov_b32 %[dkn], 1\n\t"                                                               \
-            "s_mov_b32 %[skip], 32\n\t"                                                             \
-            "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                        \
-            "s_cbranch_scc1 L%=_x1\n\t"                                                             \
-            "s_cmp_le_u32 %[lane0], %[l0max]\n\t"                                                   \
-            "s_cbranch_scc1 L%=_top\n\t"                                                            \
-            "s_branch L%=_x2\n"                                                                     \
+            K1R_V3_LEN                                                                              \
+            K1R_V2_TAIL                                                                             \
             "L%=_nohit:\n\t"                                                                        \
+            K1R_V8_SKIPFIX                                                                          \
+            K1R_V6_MWIN_NOHIT                                                                       \
             "s_bcnt1_i32_b64 %[s0], %[valid]\n\t" /* nk misses: lanes lane0 - 1 .. lane0 + nk - 1 */ \
-            "s_mov_b32 m0, %[pend]\n\t"                                                             \
-            "v_writelane_b32 %[tka], %[dka], m0\n\t"                                                \
-            "v_writelane_b32 %[tkb], %[dkb], m0\n\t"                                                \
+            K1R_V6_DRAIN                                                                            \
             "s_add_u32 %[pend], %[pend], %[dkn]\n\t"                                                \
             "s_mov_b32 %[dkn], 0\n\t"                                                               \
-            "s_mov_b32 %[dka], 0\n\t"                                                               \
-            "s_mov_b32 %[dkb], 0\n\t"                                                               \
+            K1R_V9_DKZERO                                                                           \
             "s_add_i32 %[s1], %[lane0], -1\n\t"                                                     \
             "v_subrev_u32_e32 %[t4], %[s1], %[lane]\n\t"                                            \
             "v_cmp_ge_u32_e32 vcc, %[s0], %[t4]\n\t"                                                \
@@ -907,16 +1137,13 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "ds_read_u16 %[ent], %[adr]\n\t"                                                        \
             "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"                                        \
             "s_lshr_b32 %[s3], %[s3], 5\n\t" /* the last probe steps by 2 at skip 64 */             \
-            "s_add_u32 %[p], %[q0], %[lane0]\n\t"                                                   \
-            "s_add_u32 %[p], %[p], %[s0]\n\t"                                                       \
-            "s_add_u32 %[p], %[p], %[s3]\n\t"                                                       \
-            "s_add_i32 %[p], %[p], -1\n\t"                                                          \
+            K1R_V9_NOHIT_P                                                                          \
             "s_mov_b32 %[skip], %[s2]\n\t"                                                          \
             "s_cmp_gt_u32 %[skip], %[lsmax]\n\t"                                                    \
             "s_cbranch_scc1 L%=_x1\n\t"                                                             \
             "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                        \
             "s_cbranch_scc1 L%=_x1\n\t"                                                             \
-            "s_sub_u32 %[lane0], %[p], %[q0]\n\t"                                                   \
+            K1R_V9_NOHIT_L0                                                                         \
             "s_cmp_gt_u32 %[lane0], %[l0max]\n\t"                                                   \
             "s_cbranch_scc1 L%=_x2\n\t"                                                             \
             "s_cmp_le_u32 %[skip], %[skipmax]\n\t"                                                  \
@@ -927,6 +1154,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "L%=_x4:\n\ts_mov_b32 %[code], 4\n\ts_branch L%=_end\n"                                 \
             "L%=_x5:\n\ts_mov_b32 %[code], 5\n"                                                     \
             "L%=_end:\n\t"                                                                          \
+            K1R_V8_SKIPFIX                                                                          \
             "s_mov_b32 m0, %[m0s]\n\t"                                                              \
             "s_waitcnt lgkmcnt(0)"                                                                  \
             : [p] "+s"(p), [skip] "+s"(skip), [lane0] "+s"(lane0), [pend] "+s"(pend), [dka] "+s"(dka), \
@@ -936,6 +1164,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
               [entt] "+v"(et32), [tka] "+v"(tka), [tkb] "+v"(tkb), [t0] "=&v"(_t0), [t1] "=&v"(_t1),  \
               [t2] "=&v"(_t2), [t3] "=&v"(_t3), [t4] "=&v"(_t4)                                       \
             : [q0] "s"(q0), [L] "s"(L), [lm16] "s"(L - 16), [mwin] "s"(m_win), [seghi] SEGHI,         \
+              [lim0] "s"(__builtin_elementwise_min((int32_t)(62 - SNAPPY_K1R_RMIN), (int32_t)L - 16 - (int32_t)q0)), \
+              [pdz] "s"(m_pdz),                                                                     \
               [dv] "v"(dv),                                                                         \
               [pdl1] "v"(pdl1), [pdc] "v"(pdc), [pdnz] "v"(pdnz), [adr] "v"(adr), [adrt] "v"(adr >> 1), \
               [word] "v"(word), [lane] "v"(lane), [lane4] "v"(lane << 2), [dummy] "v"(kDummy),         \

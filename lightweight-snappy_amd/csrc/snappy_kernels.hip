@@ -957,6 +957,26 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     "s_add_i32 %[p], %[p], -1\n\t"
 #define K1R_V9_NOHIT_L0 "s_sub_u32 %[lane0], %[p], %[q0]\n\t"
 #endif
+// SNAPPY_K1R_ASM_V10 (with V6): the dwords-at-pf funnel shift -8 pf by
+// v_mul_i32_i24 into a free VGPR instead of s_mul (bits 4:0 are all v_alignbit
+// reads).  (v_movrels_b32 for the candidate's register pair, which would save
+// the s_set_gpr_idx pair, does not exist on gfx950.)
+#ifndef SNAPPY_K1R_ASM_V10
+#define SNAPPY_K1R_ASM_V10 1
+#endif
+#define K1R_V10_PAIR                                                                                \
+    "s_set_gpr_idx_on %[s0], gpr_idx(SRC0)\n\t"                                                     \
+    "v_mov_b32_e32 %[t3], v2\n\t"                                                                   \
+    "v_mov_b32_e32 %[t4], v3\n\t"                                                                   \
+    "s_set_gpr_idx_off\n\t"                                                                         \
+    "s_bfe_u32 %[s1], %[c], 0x60002\n\t"
+#if SNAPPY_K1R_ASM_V10
+#define K1R_V10_SEL2A "v_mul_i32_i24_e64 %[t0], %[pf], -8\n\t"
+#define K1R_V10_FUNNEL_PA "v_alignbit_b32 %[t2], %[t2], %[t1], %[t0]\n\t"
+#else
+#define K1R_V10_SEL2A K1R_V6_SEL2A
+#define K1R_V10_FUNNEL_PA K1R_V6_FUNNEL_PA
+#endif
 #if SNAPPY_K1R_ASM_V7
 #define K1R_V7_P ""
 #undef K1R_V3_LEN
@@ -1082,12 +1102,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "ds_bpermute_b32 %[t2], %[t2], %[dv]\n\t" /* pa: dwords at pf */                        \
             K1R_V2_CMASK                                                                            \
             CAND                                                                                    \
-            "s_set_gpr_idx_on %[s0], gpr_idx(SRC0)\n\t"                                             \
-            "v_mov_b32_e32 %[t3], v2\n\t"                                                           \
-            "v_mov_b32_e32 %[t4], v3\n\t"                                                           \
-            "s_set_gpr_idx_off\n\t"                                                                 \
+            K1R_V10_PAIR                                                                            \
             WRAP                                                                                    \
-            "s_bfe_u32 %[s1], %[c], 0x60002\n\t"                                                    \
             K1R_V5_ROT                                                                              \
             K1R_V2_CA                                                                               \
             K1R_V5_SEL                                                                              \
@@ -1098,7 +1114,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "v_subrev_u32_e32 %[t4], %[s0], %[lane]\n\t"                                            \
             "s_sub_u32 %[s0], %[f], %[s0]\n\t"                                                      \
             "v_cmp_ge_u32_e32 vcc, %[s0], %[t4]\n\t" /* lanes lo0 .. f insert */                    \
-            K1R_V6_SEL2A                                                                            \
+            K1R_V10_SEL2A                                                                           \
             "v_cndmask_b32_e32 %[t4], %[dummy], %[adr], vcc\n\t"                                    \
             "ds_write_b16 %[t4], %[word]\n\t"                                                       \
             "v_lshrrev_b32_e32 %[t4], 1, %[t4]\n\t"                                                 \
@@ -1112,7 +1128,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "s_waitcnt lgkmcnt(2)\n\t" /* pa, ca and the inserts; the entry reads stay in flight */ \
             "v_mov_b32_dpp %[t1], %[t2] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
             "v_mov_b32_dpp %[t4], %[t3] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
-            K1R_V6_FUNNEL_PA                                                                        \
+            K1R_V10_FUNNEL_PA                                                                       \
             "v_perm_b32 %[t3], %[t3], %[t4], %[s3]\n\t"                                             \
             "v_cmp_ne_u32_e32 vcc, %[t2], %[t3]\n\t"                                                \
             K1R_V3_LEN                                                                              \
@@ -2215,6 +2231,11 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
     auto *const w32 = reinterpret_cast<__attribute__((address_space(3))) uint32_t *>(wb);
     uint64_t B = c0 & ~3ull;
     c1 = c0 + clen;
+    // a unit already failed by its index (an entry past the stream end) loads
+    // nothing: its window bytes [B, c0) would lie outside the stream (the
+    // guarded loads read below c1 = c0; at an entry 1 GiB past the stream end
+    // that faulted whenever the address was unmapped)
+    if (st != SNAPPY_ST_OK) B = c1 = 0;
     uint32_t ws = 0;
     // window byte x (< 512 + 8) -> LDS byte address in wb
 #define WADR(x) ({ const uint32_t _a = 256 * ws + (x); _a >= 768 ? _a - 768 : _a; })

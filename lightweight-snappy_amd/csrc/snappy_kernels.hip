@@ -977,6 +977,28 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #define K1R_V10_SEL2A K1R_V6_SEL2A
 #define K1R_V10_FUNNEL_PA K1R_V6_FUNNEL_PA
 #endif
+// SNAPPY_K1R_ASM_V11: the candidate funnel's perm selector 0x07060504 - (c % 4)
+// x 0x01010101 in VALU (and, u24 multiply, lshl_or, sub: two more VGPRs)
+// instead of s_and / s_mul / s_add
+#ifndef SNAPPY_K1R_ASM_V11
+#define SNAPPY_K1R_ASM_V11 0
+#endif
+#if SNAPPY_K1R_ASM_V11
+#define K1R_V11_SEL3                                                                                \
+    "v_and_b32_e64 %[t5], %[c], 3\n\t"                                                              \
+    "v_mul_u32_u24_e32 %[t6], 0x10101, %[t5]\n\t"                                                   \
+    "v_lshl_or_b32 %[t5], %[t6], 8, %[t5]\n\t" /* (c % 4) x 0x01010101 */                         \
+    "v_sub_u32_e32 %[t5], 0x7060504, %[t5]\n\t"
+#define K1R_V11_PERM3 "v_perm_b32 %[t3], %[t3], %[t4], %[t5]\n\t"
+#define K1R_V11_OUTS , [t5] "=&v"(_t5), [t6] "=&v"(_t6)
+#else
+#define K1R_V11_SEL3                                                                                \
+    "s_and_b32 %[s3], %[c], 3\n\t"                                                                  \
+    "s_mul_i32 %[s3], %[s3], 0xfefefeff\n\t"                                                        \
+    "s_add_i32 %[s3], %[s3], 0x7060504\n\t"
+#define K1R_V11_PERM3 "v_perm_b32 %[t3], %[t3], %[t4], %[s3]\n\t"
+#define K1R_V11_OUTS
+#endif
 #if SNAPPY_K1R_ASM_V7
 #define K1R_V7_P ""
 #undef K1R_V3_LEN
@@ -1081,7 +1103,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #endif
 #define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, CAND, SEGHI, WRAP)                                    \
     do {                                                                                            \
-        uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4;                           \
+        uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4, _t5, _t6;                 \
         uint64_t _valid, _hm, _wm;                                                                  \
         asm volatile(                                                                               \
             "s_mov_b32 %[m0s], m0\n\t"                                                              \
@@ -1122,14 +1144,12 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "ds_read_u16 %[ent], %[adr]\n\t"                                                        \
             "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"                                        \
             K1R_V6_SEL2B                                                                            \
-            "s_and_b32 %[s3], %[c], 3\n\t"                                                          \
-            "s_mul_i32 %[s3], %[s3], 0xfefefeff\n\t"                                                \
-            "s_add_i32 %[s3], %[s3], 0x7060504\n\t"                                                 \
+            K1R_V11_SEL3                                                                            \
             "s_waitcnt lgkmcnt(2)\n\t" /* pa, ca and the inserts; the entry reads stay in flight */ \
             "v_mov_b32_dpp %[t1], %[t2] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
             "v_mov_b32_dpp %[t4], %[t3] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
             K1R_V10_FUNNEL_PA                                                                       \
-            "v_perm_b32 %[t3], %[t3], %[t4], %[s3]\n\t"                                             \
+            K1R_V11_PERM3                                                                           \
             "v_cmp_ne_u32_e32 vcc, %[t2], %[t3]\n\t"                                                \
             K1R_V3_LEN                                                                              \
             K1R_V2_TAIL                                                                             \
@@ -1178,7 +1198,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
               [m0s] "=&s"(_m0s), [pf] "=&s"(_pf), [s0] "=&s"(_s0), [s1] "=&s"(_s1), [s2] "=&s"(_s2),   \
               [s3] "=&s"(_s3), [valid] "=&s"(_valid), [hm] "=&s"(_hm), [wm] "=&s"(_wm), [ent] "+v"(e32), \
               [entt] "+v"(et32), [tka] "+v"(tka), [tkb] "+v"(tkb), [t0] "=&v"(_t0), [t1] "=&v"(_t1),  \
-              [t2] "=&v"(_t2), [t3] "=&v"(_t3), [t4] "=&v"(_t4)                                       \
+              [t2] "=&v"(_t2), [t3] "=&v"(_t3), [t4] "=&v"(_t4) K1R_V11_OUTS                          \
             : [q0] "s"(q0), [L] "s"(L), [lm16] "s"(L - 16), [mwin] "s"(m_win), [seghi] SEGHI,         \
               [lim0] "s"(__builtin_elementwise_min((int32_t)(62 - SNAPPY_K1R_RMIN), (int32_t)L - 16 - (int32_t)q0)), \
               [pdz] "s"(m_pdz),                                                                     \
@@ -1754,6 +1774,11 @@ __device__ __forceinline__ void k2_long_literals(uint8_t *w, const uint8_t *__re
     }
 }
 
+// measurement only (wrong output): K2 reads no literal bytes from the input, the
+// upper bound of what literals staged by K1r could save K2
+#ifndef SNAPPY_K2_NOLIT
+#define SNAPPY_K2_NOLIT 0
+#endif
 // 1: no register cap (80 VGPRs, 6 waves/SIMD with 128-token passes); capping at
 // 7 or 8 waves spills and measured slower (1.18 / 1.22 against 0.979
 // ms of K3 + K2 per GiB of text)
@@ -1847,7 +1872,7 @@ __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(cons
 #pragma unroll
     for (uint32_t i = 0; i < kK2Per; i++) {
         wide[i] = base + pe[i] + 20 <= n;  // the aligned 20-byte read ends inside in[0, n)
-        const bool ld = staged && wide[i] && live[i] && litn[i] != 0 && litn[i] <= 16;
+        const bool ld = !SNAPPY_K2_NOLIT && staged && wide[i] && live[i] && litn[i] != 0 && litn[i] <= 16;
         const uintptr_t sa = reinterpret_cast<uintptr_t>(src + pe[i]);
         lsh[i] = (uint32_t)(sa & 3);
         const auto *aw = reinterpret_cast<const __attribute__((address_space(1))) uint32_t *>(
@@ -1866,7 +1891,7 @@ __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(cons
         rel += sz[i];
     }
 #pragma unroll
-    for (uint32_t i = 0; i < kK2Per; i++) {
+    for (uint32_t i = 0; i < kK2Per && !SNAPPY_K2_NOLIT; i++) {
         if (staged) k2_long_literals(stage, src, longs[i], litn[i], pe[i], d0v[i], lane);
         else k2_long_literals(dst + o, src, in + n, longs[i], litn[i], pe[i], d0v[i], lane);
     }
@@ -2339,6 +2364,11 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
 #ifndef SNAPPY_K4_PACKED_SCAN
 #define SNAPPY_K4_PACKED_SCAN 1
 #endif
+// SNAPPY_K4_BPL4 (A/B): byte passes of 256 output bytes, four per lane (one
+// ring dword per lane, passes on 4-aligned output positions): see the pass loop
+#ifndef SNAPPY_K4_BPL4
+#define SNAPPY_K4_BPL4 0
+#endif
     // the last batch was cut by the 1,024-byte output span (long copies): parse one
     // half only -- more elements would be cut again (repeat-like data)
     bool span_cut = false;
@@ -2602,7 +2632,9 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             // op_end) too: a batch starts with op - F < 2048 (the flush below),
             // and 2048 + kK4MapBits <= ring - 64
             static_assert(2048 + kK4MapBits <= kK4Ring - 64, "K4: the ring must hold [F, op_end)");
-            const uint64_t over = __ballot(lane < nexec && lane > 0 && out_off + e_len > kK4MapBits);
+            // (four bytes per lane: the map starts at op & ~3, so op & 3 bits fewer)
+            const uint64_t over = __ballot(lane < nexec && lane > 0 &&
+                                           out_off + e_len > kK4MapBits - (SNAPPY_K4_BPL4 ? (op & 3) : 0u));
 #ifdef SNAPPY_K4_STATS
             const uint32_t nexec_l = nexec;
 #endif
@@ -2649,9 +2681,10 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             // LDS operations complete in issue order, so only the compiler could
             // reorder the clear, the or and the read; lanes w and w + 32 store
             // the same zero into dword w)
+            const uint32_t mh = SNAPPY_K4_BPL4 ? (op & 3) : 0u;  // the map's bit 0 = output byte op - mh
             map32[lane & 31] = 0;
             asm volatile("" ::: "memory");
-            if (ex) __hip_atomic_fetch_or(map32 + (out_off >> 5), 1u << (out_off & 31), __ATOMIC_RELAXED,
+            if (ex) __hip_atomic_fetch_or(map32 + ((out_off + mh) >> 5), 1u << ((out_off + mh) & 31), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WORKGROUP);
             asm volatile("" ::: "memory");
             const uint32_t bm = map32[lane & 31];
@@ -2662,6 +2695,9 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             // 32 KiB streams and 1.3 % on 64 KiB blocks: profiles/r04a_ab_k4_*, r04b_ab_k4_*)
             const uint32_t kop = e_op | (e_t == 0 ? 0x80000000u : 0u);
             const uint32_t kinfo = e_t == 0 ? (256 * ws + e_lsrc) ^ 0x80000000u : e_info;
+#if SNAPPY_K4_BPL4
+            K4_PASSES_BPL4
+#else
             uint32_t cb = 0;  // elements starting before the pass
             // pass P: byte lane l writes output byte o = P + l
             for (uint32_t P = op, i = 0; P < op_end; P += 64, i++) {
@@ -2745,6 +2781,7 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 n_sub++;
 #endif
             }
+#endif
         }
         K4STAMP(td);
 #ifdef SNAPPY_K4_STATS

@@ -2364,6 +2364,13 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
 #ifndef SNAPPY_K4_PACKED_SCAN
 #define SNAPPY_K4_PACKED_SCAN 1
 #endif
+// SNAPPY_K4_PASS_V2 (pass 1): a byte's address from one per-element value, kx =
+// the literal's window address - its output start, or - the copy offset: t = o +
+// kx is the window address (literal) or the source (copy); a copy overlaps its
+// own output iff t >= its start (d >= off), far iff t < lo
+#ifndef SNAPPY_K4_PASS_V2
+#define SNAPPY_K4_PASS_V2 1
+#endif
 // SNAPPY_K4_BPL4 (A/B): byte passes of 256 output bytes, four per lane (one
 // ring dword per lane, passes on 4-aligned output positions): see the pass loop
 #ifndef SNAPPY_K4_BPL4
@@ -2696,9 +2703,178 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             const uint32_t kop = e_op | (e_t == 0 ? 0x80000000u : 0u);
             const uint32_t kinfo = e_t == 0 ? (256 * ws + e_lsrc) ^ 0x80000000u : e_info;
 #if SNAPPY_K4_BPL4
-            K4_PASSES_BPL4
+            // four output bytes per lane: pass P covers [P, P + 256) from P0 = op & ~3,
+            // lane l owns ring dword (P + 4l) & M.  Bytes below op and from op_end on
+            // are kept (written back with the ring's own value).  A byte's element:
+            // the starts before the lane's first byte (whole map dwords below, by one
+            // scan per batch, + the bits below it in its dword) and those in its
+            // nibble.  Elements of bytes 0 and 1 are e0 or e0 + 1, looked up for every
+            // lane; bytes 2 and 3 of a lane with two or more starts in bytes 1..3 look
+            // theirs up (a uniform branch on the ballot)
+            const uint32_t P0 = op - mh;
+            const uint32_t pcn = (uint32_t)__builtin_popcount(bm);  // lanes >= 32 repeat 0..31
+            uint32_t cx = pcn;
+            cx += dpp0<0x111, 0xF>(cx);
+            cx += dpp0<0x112, 0xF>(cx);
+            cx += dpp0<0x114, 0xF>(cx);
+            cx += dpp0<0x118, 0xF>(cx);
+            cx += dpp0<0x142, 0xA>(cx);
+            cx -= pcn;  // lanes 0..31: the starts in map dwords below the lane's
+            const uint32_t nsh = 4 * (lane & 7);
+            const uint32_t lmask = (1u << nsh) - 1;
+            for (uint32_t P = P0, i = 0; P < op_end; P += 256, i++) {
+                const int wa = (int)(4 * (8 * i + (lane >> 3)));
+                const uint32_t dw = (uint32_t)__builtin_amdgcn_ds_bpermute(wa, (int)bm);
+                const uint32_t cnt = (uint32_t)__builtin_amdgcn_ds_bpermute(wa, (int)cx);
+                const uint32_t nib = (dw >> nsh) & 15;
+                const uint32_t e0 = (uint32_t)__builtin_popcount(dw & lmask) + cnt + (nib & 1) - 1;
+                const uint32_t F0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(e0 << 2), (int)kop);
+                const uint32_t I0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(e0 << 2), (int)kinfo);
+                const uint32_t F1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((e0 + 1) << 2), (int)kop);
+                const uint32_t I1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((e0 + 1) << 2), (int)kinfo);
+                const bool multi = __ballot(__builtin_popcount(nib & 14) >= 2) != 0;
+                const uint32_t o0 = P + 4 * lane;
+                uint32_t wv = 0;
+                SrcT srcb[4];
+                bool inp[4];
+#pragma unroll
+                for (uint32_t b = 0; b < 4; b++) {
+                    const uint32_t o = o0 + b;
+                    const uint32_t kb = (uint32_t)__builtin_popcount(nib & (14u & ((2u << b) - 1)));
+                    uint32_t f_op = kb ? F1 : F0, f_in = kb ? I1 : I0;
+                    if (b >= 2 && multi) {
+                        const int ea = (int)((e0 + kb) << 2);
+                        const uint32_t g_op = (uint32_t)__builtin_amdgcn_ds_bpermute(ea, (int)kop);
+                        const uint32_t g_in = (uint32_t)__builtin_amdgcn_ds_bpermute(ea, (int)kinfo);
+                        f_op = kb >= 2 ? g_op : f_op;
+                        f_in = kb >= 2 ? g_in : f_in;
+                    }
+                    const uint32_t d = o - f_op;  // a literal's carries 2^31, cancelled by its kinfo
+                    const bool lit = (int32_t)f_op < 0;
+                    const bool pend = o >= op && o < op_end;
+                    SrcT src = (SrcT)o - (SrcT)f_in;
+                    bool far = pend && !lit && src < (SrcT)lo;
+                    uint32_t fv = 0;
+#ifndef SNAPPY_K4_NOFAR
+                    if (far) fv = dst[src];
+#endif
+                    uint32_t a = f_in + d;
+                    const uint32_t a2 = a - 768;
+                    a = a < a2 ? a : a2;
+                    const uint32_t lb = wb[a < 783 ? a : 783];
+                    if (pend && !lit && !far && d >= f_in) {
+                        // overlapping copy (off < len <= 64): source byte d mod off
+                        const float r = __builtin_amdgcn_rcpf((float)f_in);
+                        const uint32_t qd = (uint32_t)((float)d * r + 0.0001f);
+                        src = (SrcT)f_op - (SrcT)f_in + (SrcT)(d - qd * f_in);
+                        if constexpr (BACK) {
+                            if (src < (SrcT)lo) {
+                                fv = dst[src];
+                                far = true;
+                            }
+                        }
+                    }
+#ifdef SNAPPY_K4_STATS
+                    n_far += (b == 0 && __ballot(far) != 0) ? 1u : 0u;
+#endif
+                    inp[b] = pend && !lit && !far && src >= (SrcT)P;
+                    srcb[b] = pend ? src : (SrcT)o;
+                    const uint8_t rv = ob[(uint32_t)srcb[b] & M];
+                    const uint8_t lr = (pend && lit) ? (uint8_t)lb : rv;
+                    const uint32_t v = far ? fv : (uint32_t)lr;
+                    wv |= (v & 0xFF) << (8 * b);
+                }
+                auto *const od = reinterpret_cast<uint32_t *>(ob + (o0 & M));
+                *od = wv;
+#ifdef SNAPPY_K4_STATS
+                n_pass++;
+                n_sub++;
+#endif
+                if (__builtin_expect(__ballot(inp[0] || inp[1] || inp[2] || inp[3]) != 0, 0)) {
+                    // sources inside this pass (each below its byte: a copy's source, mapped
+                    // mod off for overlapping copies, lies before the copy): re-read them
+                    // until nothing changes.  Every round reads what the last one wrote
+                    // (one wave's LDS operations complete in order), and the only fixed
+                    // point of an acyclic system is its solution
+                    for (;;) {
+                        uint32_t nv = wv;
+#pragma unroll
+                        for (uint32_t b = 0; b < 4; b++) {
+                            const uint32_t r = ob[(uint32_t)srcb[b] & M];
+                            nv = inp[b] ? ((nv & ~(0xFFu << (8 * b))) | (r << (8 * b))) : nv;
+                        }
+#ifdef SNAPPY_K4_STATS
+                        n_sub++;
+#endif
+                        if (!__ballot(nv != wv)) break;
+                        *od = nv;
+                        wv = nv;
+                    }
+                }
+            }
 #else
             uint32_t cb = 0;  // elements starting before the pass
+#if SNAPPY_K4_PASS_V2
+            if constexpr (!BACK) {
+            const uint32_t kx = e_t == 0 ? 256 * ws + e_lsrc - e_op : 0u - e_info;
+            for (uint32_t P = op, i = 0; P < op_end; P += 64, i++) {
+                const uint64_t sm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(bm, 2 * i + 1) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane(bm, 2 * i);
+                const uint64_t sm1 = sm >> 1;
+                const uint32_t id = __builtin_amdgcn_mbcnt_hi(
+                    (uint32_t)(sm1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm1, cb - 1 + (uint32_t)(sm & 1)));
+                cb += (uint32_t)__builtin_popcountll(sm);
+                const uint32_t f_op = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)kop);
+                const uint32_t f_x = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)kx);
+                const uint32_t o = P + lane;
+                const bool lit = (int32_t)f_op < 0;
+                const bool pend = o < op_end;
+                uint32_t t = o + f_x;
+                const bool far = pend && !lit && t < lo;
+                uint32_t fv;
+                asm volatile("" : "=v"(fv));  // (no initial value: read only where far)
+#ifndef SNAPPY_K4_NOFAR
+                if (far) fv = dst[t];
+#endif
+                const uint32_t a2 = t - 768;
+                const uint32_t lb = wb[__builtin_elementwise_min(__builtin_elementwise_min(t, a2), 783u)];
+                if (pend && !lit && !far && t >= f_op) {
+                    // overlapping copy (off < len <= 64): source byte d mod off
+                    const uint32_t off = 0u - f_x, d = o - f_op;
+                    const float r = __builtin_amdgcn_rcpf((float)off);
+                    const uint32_t qd = (uint32_t)((float)d * r + 0.0001f);
+                    t = f_op - off + (d - qd * off);
+                }
+#ifdef SNAPPY_K4_STATS
+                n_far += __ballot(far) != 0;
+                n_pass++;
+#endif
+                // a source in this pass: copy lanes' t (< 2^31), -1 elsewhere (one compare
+                // for the ballot: a ballot of the and of the conditions went through a
+                // 0 / 1 VGPR and a second compare)
+                const int32_t tin = (pend && !lit && !far) ? (int32_t)t : -1;
+                const uint8_t rv = ob[t & M];
+                const uint8_t lr = lit ? (uint8_t)lb : rv;
+                uint32_t val = far ? fv : (uint32_t)lr;
+                if (__builtin_expect(__ballot(tin >= (int32_t)P) != 0, 0)) {
+                    uint32_t rt = tin >= (int32_t)P ? t - P : lane;
+                    for (;;) {
+#ifdef SNAPPY_K4_STATS
+                        n_sub++;
+#endif
+                        const uint32_t r2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rt << 2), (int)rt);
+                        if (!__ballot(r2 != rt)) break;
+                        rt = r2;
+                    }
+                    val = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rt << 2), (int)val);
+                }
+                ob[pend ? (o & M) : kK4Ring] = (uint8_t)val;
+#ifdef SNAPPY_K4_STATS
+                n_sub++;
+#endif
+            }
+            } else
+#endif
             // pass P: byte lane l writes output byte o = P + l
             for (uint32_t P = op, i = 0; P < op_end; P += 64, i++) {
                 const uint64_t sm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(bm, 2 * i + 1) << 32) |

@@ -109,7 +109,7 @@ typedef uint32_t v32 __attribute__((ext_vector_type(32)));
 typedef uint32_t __attribute__((aligned(1))) u32u;
 typedef uint16_t __attribute__((aligned(1))) u16u;
 
-constexpr uint32_t kTagMul = 0x9E3779B1u;
+[[maybe_unused]] constexpr uint32_t kTagMul = 0x9E3779B1u;
 constexpr uint32_t kRegs = 128;  // VGPRs holding a 32 KiB unit (64 dwords each), + 1 zero spare
 // Register r (wave-uniform) of the resident unit.  g0..g3 are pinned to
 // v2..v129 by the asm constraints, so the relative move (s_set_gpr_idx_on,
@@ -290,13 +290,23 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
 #endif
 
 
-#if defined(SNAPPY_K1R_LSTAMPS)
+#if defined(SNAPPY_K1R_LSTAMPS) || defined(SNAPPY_K1R_RSTAMPS)
 #define MSTAMP(var)                                                                         \
     do {                                                                                    \
         __builtin_amdgcn_sched_barrier(0);                                                  \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory");        \
         __builtin_amdgcn_sched_barrier(0);                                                  \
     } while (0)
+#endif
+// SNAPPY_K1R_RSTAMPS (measurement build): the window refresh's cycles (token
+// flush and window move separately) against the whole loop's, with the asm
+// round loop in place (the LSTAMPS / STATS builds run the C++ round instead)
+#if defined(SNAPPY_K1R_RSTAMPS)
+#define RSTAMP(var) MSTAMP(var)
+#else
+#define RSTAMP(var) do { } while (0)
+#endif
+#if defined(SNAPPY_K1R_LSTAMPS)
 #define LSTAMP(var) MSTAMP(var)
 #define LSEG(i, a, b) seg[i] += (b) - (a)
 #else
@@ -419,7 +429,18 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #define TBL_READ(h) TBL_READ3(2 * (h))
 #define TBL_WRITE(s, word) TBL_WRITE3(2 * (s), word)
 #endif
+// SNAPPY_K1R_TAG1: the tag as the 8 product bits below the table index, ((v *
+// kMul) >> (shift - 8)) & 0xFF, instead of a second multiply (any function of
+// the 4 bytes filters candidates: equal bytes give equal tags, and a tag
+// collision is verified like any hit)
+#ifndef SNAPPY_K1R_TAG1
+#define SNAPPY_K1R_TAG1 1
+#endif
+#if SNAPPY_K1R_TAG1
+#define TAG_OF(v) __builtin_amdgcn_ubfe((v) * kMul, shift - 8, 8)
+#else
 #define TAG_OF(v) (((v) * kTagMul) >> 24)
+#endif
 // an insert group: the lanes where cond holds write their record; the others
 // write the dummy record (one instruction stream, no exec change: masking
 // them off measured 3 % slower, profiles/r03j_ab_k1r_masked_*)
@@ -618,11 +639,24 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         const uint32_t _a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_k << 2), (int)dv);       \
         const uint32_t _b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_k + 1) << 2), (int)dv); \
         bv = funnel_bytes(_a, _b, perm_sel((q0 + lane) & 3));                                     \
-        hv = ((bv * kMul) >> shift) | (TAG_OF(bv) << 16);                                          \
+        if (SNAPPY_K1R_TAG1) {                                                                     \
+            const uint32_t _pr = bv * kMul;                                                        \
+            hv = (_pr >> shift) | (__builtin_amdgcn_ubfe(_pr, shift - 8, 8) << 16);                \
+        } else {                                                                                   \
+            hv = ((bv * kMul) >> shift) | (TAG_OF(bv) << 16);                                      \
+        }                                                                                          \
     } while (0)
+// SNAPPY_K1R_WIN_ENT: a window refresh reads the new window's table entries as
+// soon as the addresses are known (their LDS round trip overlaps the lane data)
+// instead of after it
+#ifndef SNAPPY_K1R_WIN_ENT
+#define SNAPPY_K1R_WIN_ENT 1
+#endif
 #define WINDOW_LS(qq)                                                                              \
     do {                                                                                           \
         WINDOW_AT(qq);                                                                             \
+        adr = TBL_ADR(hv & 0xFFFF);                                                                \
+        if (SNAPPY_K1R_WIN_ENT) TBL_READ_ENT(adr); /* in flight during the lane data below */     \
         const uint32_t _bits = same_x_bits<DMAX>((hv & 0xFFFF) + 1);                               \
         const uint32_t _pd = _bits ? (uint32_t)__builtin_ctz(_bits) : 0u;                          \
         /* lane - pd + 1, or lane - 1 at pd = 1: pdl1 >= lane0 also implies lane > lane0 */      \
@@ -636,7 +670,6 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         const bool _inw = (int32_t)lane <= _w16 && lane <= 62;                                     \
         m_win = __ballot(_inw);                                                                    \
         m_win17 = __ballot((int32_t)lane <= _w17 && lane <= 62);                                   \
-        adr = TBL_ADR(hv & 0xFFFF);                                                                \
         word = (q0 + lane) | (hv & 0xFF0000u);                                                     \
         if (SNAPPY_K1R_ASM_V6 && !_inw) { /* the asm hit test sees the window mask in the lane data */ \
             word |= 1u << 24;                                                                      \
@@ -701,6 +734,11 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         dkn = 0;
     };
 
+#ifdef SNAPPY_K1R_RSTAMPS
+    const uint64_t t_loop = clock64();
+    uint64_t rs_flush = 0, rs_win = 0, rs_asm = 0;
+    uint32_t rs_n = 0, rs_nfl = 0, rs_nasm = 0, rs_code[6] = {0, 0, 0, 0, 0, 0};
+#endif
 #ifdef SNAPPY_K1R_STATS
     const uint64_t t_loop = clock64();
     uint32_t n_probe = 0, n_match = 0, n_round = 0, n_refresh = 0;
@@ -1104,6 +1142,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, CAND, SEGHI, WRAP)                                    \
     do {                                                                                            \
         uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4, _t5, _t6;                 \
+        (void)_t5;                                                                                  \
+        (void)_t6;                                                                                  \
         uint64_t _valid, _hm, _wm;                                                                  \
         asm volatile(                                                                               \
             "s_mov_b32 %[m0s], m0\n\t"                                                              \
@@ -1229,6 +1269,30 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #ifdef SNAPPY_K1R_STATS
                 n_refresh++;
 #endif
+#ifdef SNAPPY_K1R_RSTAMPS
+                uint64_t r0, r1, r2;
+                const bool rfl = pend + dkn > 48;
+                if constexpr (BIG) {  // (the product's order: the move first, see below)
+                    RSTAMP(r0);
+                    WINDOW_LS(p - 1);
+                    RSTAMP(r1);
+                    if (rfl) flush_tokens();
+                    RSTAMP(r2);
+                    rs_win += r1 - r0;
+                    rs_flush += r2 - r1;
+                } else {
+                    RSTAMP(r0);
+                    if (rfl) flush_tokens();
+                    RSTAMP(r1);
+                    WINDOW_LS(p - 1);
+                    RSTAMP(r2);
+                    rs_flush += r1 - r0;
+                    rs_win += r2 - r1;
+                }
+                rs_n++;
+                rs_nfl += rfl;
+                if (false)
+#endif
                 // the deferred token stays pending (drained by the next round): count it.
                 // BIG: the window move waits vmcnt(0) for its staged LDS-DMA, and vmcnt
                 // counts stores too (in issue order): flush after the move, so that
@@ -1248,9 +1312,11 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 LSEG(5, s5, s6);
             };
             uint32_t lane0 = p - q0;
+            bool went = false;
             if (!lsw || lane0 + SNAPPY_K1R_RMIN > 62) {
                 refresh();
                 lane0 = 1;
+                went = SNAPPY_K1R_WIN_ENT;
             }
             // the round's table entries: read right after the round's inserts, so the
             // read is in flight during the verification (each path that writes the table
@@ -1259,24 +1325,34 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             // where it is issued (round 3: that wait made this order 8 % slower; now
             // text32k 16.19 -> 16.18 ms, 64 KiB blocks 19.37 -> 19.20, profiles/r03s2b_*;
             // SNAPPY_K1R_LATE_ENT reads at the round's end instead)
-            TBL_READ_ENT(adr);
+            if (!went) TBL_READ_ENT(adr);
             for (;;) {
 #if K1R_ASM_ROUNDS
                 if constexpr (!BIG || SNAPPY_K1R_ASM_BIG) {
                     // the common rounds as one hand-scheduled loop (k1r_asm_rounds below)
                     uint32_t code, fx, cx;
                     uint32_t e32 = ent, et32 = ent_t;
+#ifdef SNAPPY_K1R_RSTAMPS
+                    uint64_t ra0, ra1;
+                    RSTAMP(ra0);
+#endif
                     if constexpr (BIG)
                         K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND64, K1R_SEGHI64(seg_hi), K1R_WRAP64);
                     else
                         K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND32, "i"(0), "");
+#ifdef SNAPPY_K1R_RSTAMPS
+                    RSTAMP(ra1);
+                    rs_asm += ra1 - ra0;
+                    rs_nasm++;
+                    rs_code[code < 6 ? code : 0]++;
+#endif
                     ent = (uint16_t)e32;
                     ent_t = (uint8_t)et32;
                     if (code == 1) break;  // skip past the step-1 range, or is_block_end
                     if (code == 2) {       // the window needs to move
                         refresh();
                         lane0 = 1;
-                        TBL_READ_ENT(adr);
+                        if (!SNAPPY_K1R_WIN_ENT) TBL_READ_ENT(adr);
                         continue;
                     }
                     if (code >= 4) {  // the round stopped after its inserts: finish it here
@@ -1305,7 +1381,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                         if (lane0 + SNAPPY_K1R_RMIN > 62) {
                             refresh();
                             lane0 = 1;
-                            TBL_READ_ENT(adr);
+                            if (!SNAPPY_K1R_WIN_ENT) TBL_READ_ENT(adr);
                         }
                         continue;
                     }
@@ -1424,7 +1500,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     refresh();
                     lane0 = 1;
 #ifndef SNAPPY_K1R_LATE_ENT
-                    TBL_READ_ENT(adr);
+                    if (!SNAPPY_K1R_WIN_ENT) TBL_READ_ENT(adr);
 #endif
                 }
 #ifdef SNAPPY_K1R_LATE_ENT
@@ -1527,6 +1603,15 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         ntok_out[u] = nt;
         sizes[u] = acc + (L > cend ? literal_bytes(L - cend) : 0u);
     }
+#ifdef SNAPPY_K1R_RSTAMPS
+    if (lane == 0) {
+        uint64_t *st = reinterpret_cast<uint64_t *>(tokens + (uint64_t)gridDim.x * tok_cap) + 4 * (uint64_t)u;
+        st[0] = clock64() - t_loop;
+        st[1] = rs_flush | (rs_asm << 24);  // (a unit's flush cycles < 2^24)
+        st[2] = rs_win | ((uint64_t)rs_nasm << 40);
+        st[3] = rs_n | ((uint64_t)rs_nfl << 16) | ((uint64_t)rs_code[3] << 32) | ((uint64_t)(rs_code[4] + rs_code[5]) << 48);
+    }
+#endif
 #ifdef SNAPPY_K1R_STATS
     if (lane == 0) {
         uint64_t *st = reinterpret_cast<uint64_t *>(tokens + (uint64_t)gridDim.x * tok_cap) + 4 * (uint64_t)u;
@@ -2197,7 +2282,10 @@ constexpr uint32_t kK4MapBits = 1024; // a batch's output span (bit j = an eleme
 constexpr uint32_t kK4MapAt = 784;    // after the window: 3 x 256 bytes + a 16-byte mirror
 constexpr uint32_t kK4TailAt = kK4MapAt + kK4MapBits / 8;
 constexpr uint32_t kK4RingAt = kK4TailAt + 16;
-constexpr uint32_t kK4Lds = kK4RingAt + kK4Ring + 4;  // 5,028 B: 32 waves per CU fit 160 KiB
+#ifndef SNAPPY_K4_LDS_PAD
+#define SNAPPY_K4_LDS_PAD 0  // (measurement: pad the LDS to run fewer waves per CU)
+#endif
+constexpr uint32_t kK4Lds = kK4RingAt + kK4Ring + 4 + SNAPPY_K4_LDS_PAD;  // 5,028 B: 32 waves per CU fit 160 KiB
 
 template <bool BACK>
 __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const uint64_t *__restrict__ offsets,
@@ -2370,6 +2458,10 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
 // own output iff t >= its start (d >= off), far iff t < lo
 #ifndef SNAPPY_K4_PASS_V2
 #define SNAPPY_K4_PASS_V2 1
+#endif
+// SNAPPY_K4_PASS_PIPE (with V2): passes software-pipelined by one stage
+#ifndef SNAPPY_K4_PASS_PIPE
+#define SNAPPY_K4_PASS_PIPE 0
 #endif
 // SNAPPY_K4_BPL4 (A/B): byte passes of 256 output bytes, four per lane (one
 // ring dword per lane, passes on 4-aligned output positions): see the pass loop
@@ -2814,7 +2906,79 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             }
 #else
             uint32_t cb = 0;  // elements starting before the pass
-#if SNAPPY_K4_PASS_V2
+#if SNAPPY_K4_PASS_V2 && SNAPPY_K4_PASS_PIPE
+            if constexpr (!BACK) {
+            const uint32_t kx = e_t == 0 ? 256 * ws + e_lsrc - e_op : 0u - e_info;
+            // software-pipelined passes: stage A of pass i + 1 (element lookup, address,
+            // far load, window byte -- nothing that reads the ring) is issued before stage
+            // B of pass i (ring read, in-pass fix-up, ring write), so its LDS and memory
+            // latencies overlap pass i's work (K4 runs ~8 % slower per wave removed
+            // from a SIMD: it is latency-bound, profiles/r05s_ab_kb-k4o7-k4o6_*)
+            struct PassA {
+                uint32_t f_op, t, lb, fv;
+                bool lit, pend, far;
+            };
+            auto stage_a = [&](uint32_t P, uint32_t i, PassA &s) {
+                const uint64_t sm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(bm, 2 * i + 1) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane(bm, 2 * i);
+                const uint64_t sm1 = sm >> 1;
+                const uint32_t id = __builtin_amdgcn_mbcnt_hi(
+                    (uint32_t)(sm1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm1, cb - 1 + (uint32_t)(sm & 1)));
+                cb += (uint32_t)__builtin_popcountll(sm);
+                s.f_op = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)kop);
+                const uint32_t f_x = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)kx);
+                const uint32_t o = P + lane;
+                s.lit = (int32_t)s.f_op < 0;
+                s.pend = o < op_end;
+                uint32_t t = o + f_x;
+                s.far = s.pend && !s.lit && t < lo;
+                asm volatile("" : "=v"(s.fv));  // (no initial value: read only where far)
+#ifndef SNAPPY_K4_NOFAR
+                if (s.far) s.fv = dst[t];
+#endif
+                const uint32_t a2 = t - 768;
+                s.lb = wb[__builtin_elementwise_min(__builtin_elementwise_min(t, a2), 783u)];
+                if (s.pend && !s.lit && !s.far && t >= s.f_op) {
+                    const uint32_t off = 0u - f_x, d = o - s.f_op;
+                    const float r = __builtin_amdgcn_rcpf((float)off);
+                    const uint32_t qd = (uint32_t)((float)d * r + 0.0001f);
+                    t = s.f_op - off + (d - qd * off);
+                }
+                s.t = t;
+            };
+            PassA cur, nxt;
+            stage_a(op, 0, cur);
+            for (uint32_t P = op, i = 0; P < op_end; P += 64, i++) {
+                if (P + 64 < op_end) stage_a(P + 64, i + 1, nxt);
+                const uint32_t o = P + lane;
+#ifdef SNAPPY_K4_STATS
+                n_far += __ballot(cur.far) != 0;
+                n_pass++;
+#endif
+                const int32_t tin = (cur.pend && !cur.lit && !cur.far) ? (int32_t)cur.t : -1;
+                const uint8_t rv = ob[cur.t & M];
+                const uint8_t lr = cur.lit ? (uint8_t)cur.lb : rv;
+                uint32_t val = cur.far ? cur.fv : (uint32_t)lr;
+                if (__builtin_expect(__ballot(tin >= (int32_t)P) != 0, 0)) {
+                    uint32_t rt = tin >= (int32_t)P ? cur.t - P : lane;
+                    for (;;) {
+#ifdef SNAPPY_K4_STATS
+                        n_sub++;
+#endif
+                        const uint32_t r2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rt << 2), (int)rt);
+                        if (!__ballot(r2 != rt)) break;
+                        rt = r2;
+                    }
+                    val = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rt << 2), (int)val);
+                }
+                ob[cur.pend ? (o & M) : kK4Ring] = (uint8_t)val;
+#ifdef SNAPPY_K4_STATS
+                n_sub++;
+#endif
+                cur = nxt;
+            }
+            } else
+#elif SNAPPY_K4_PASS_V2
             if constexpr (!BACK) {
             const uint32_t kx = e_t == 0 ? 256 * ws + e_lsrc - e_op : 0u - e_info;
             for (uint32_t P = op, i = 0; P < op_end; P += 64, i++) {

@@ -182,6 +182,10 @@ for step in "$@"; do
             rc=$?; echo "e2e '$o' rc=$rc"; [ $rc -ne 0 ] && exit $rc
         done; done
         python3 -c "import json,sys; [print(d['ms_per_step'], d['value'], d['value_end_to_end'], d['exchange']['end_to_end_ms_per_step'], d['exchange']['end_to_end_step'][-40:], d['round_trip_ok']) for d in map(json.loads, [l for l in open(sys.argv[1]) if l.startswith('{')])]" "$out/e2e_$tb.json" ;;
+    rst:*)  # rst:<chunk> -> K1r / K1r64 refresh share with the asm loop (SNAPPY_K1R_RSTAMPS build, variant rst), 256 MiB
+        IFS=: read -r _ chunk <<< "$step"
+        timeout -k 10 200 python -u tools/k1r_rstamps.py 268435456 $chunk rst > "$out/rst_$chunk.log" 2>&1
+        rc=$?; echo "rst rc=$rc"; cat "$out/rst_$chunk.log"; [ $rc -ne 0 ] && exit $rc ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -2277,7 +2277,14 @@ static __device__ uint64_t g_k4_stats[16];  // (k4_body is parsed, never instant
 // K4's LDS (static, so every base folds into a ds offset field): the
 // compressed window at 0 (ds_read2 has only 8-bit dword offsets), the batch's
 // element-start bitmap, two scalars, the output ring and one dummy byte
-constexpr uint32_t kK4Ring = 4096;    // output ring; copies reaching further back read HBM
+#ifndef SNAPPY_K4_RING
+#define SNAPPY_K4_RING 4096
+#endif
+constexpr uint32_t kK4Ring = SNAPPY_K4_RING;  // output ring; copies reaching further back read HBM
+// the ring is flushed to HBM when op - F reaches kK4FlushAt, up to a multiple of
+// kK4FlushGran (a batch then starts with op - F < kK4FlushAt)
+constexpr uint32_t kK4FlushAt = kK4Ring >= 4096 ? 2048 : 512;
+constexpr uint32_t kK4FlushGran = kK4Ring >= 4096 ? 1024 : 512;
 constexpr uint32_t kK4MapBits = 1024; // a batch's output span (bit j = an element starts at op + j)
 constexpr uint32_t kK4MapAt = 784;    // after the window: 3 x 256 bytes + a 16-byte mirror
 constexpr uint32_t kK4TailAt = kK4MapAt + kK4MapBits / 8;
@@ -2728,9 +2735,9 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
         if (nexec && !(longm && (longm & 1))) {
             // the bitmap must hold the batch's output: cut the batch (never below
             // one element: the first is <= 508 bytes).  The ring then holds [F,
-            // op_end) too: a batch starts with op - F < 2048 (the flush below),
-            // and 2048 + kK4MapBits <= ring - 64
-            static_assert(2048 + kK4MapBits <= kK4Ring - 64, "K4: the ring must hold [F, op_end)");
+            // op_end) too: a batch starts with op - F < kK4FlushAt (the flush below),
+            // and kK4FlushAt + kK4MapBits <= ring - 64
+            static_assert(kK4FlushAt + kK4MapBits <= kK4Ring - 64, "K4: the ring must hold [F, op_end)");
             // (four bytes per lane: the map starts at op & ~3, so op & 3 bits fewer)
             const uint64_t over = __ballot(lane < nexec && lane > 0 &&
                                            out_off + e_len > kK4MapBits - (SNAPPY_K4_BPL4 ? (op & 3) : 0u));
@@ -3135,8 +3142,8 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             ip += __builtin_amdgcn_readlane(in_off, nexec - 1) + __builtin_amdgcn_readlane(e_size, nexec - 1);
             op += __builtin_amdgcn_readlane(out_off, nexec - 1) + __builtin_amdgcn_readlane(e_len, nexec - 1);
             op = op < want ? op : want;
-            if (op - F >= 2048) {
-                const uint32_t T = op & ~1023u;
+            if (op - F >= kK4FlushAt) {
+                const uint32_t T = op & ~(kK4FlushGran - 1);
                 k4_flush(ob, M, dst, F, T, lane);
                 F = T;
                 if constexpr (BACK) k4_publish(status, u, SNAPPY_ST_DEFER + (int32_t)F, lane);

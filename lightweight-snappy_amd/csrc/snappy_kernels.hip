@@ -1859,6 +1859,14 @@ __device__ __forceinline__ void k2_long_literals(uint8_t *w, const uint8_t *__re
     }
 }
 
+// SNAPPY_K2_PREFETCH: token words one pass ahead (see the pass loop)
+// (A/B on 1 GiB, outputs identical, profiles/r05u_ab_k2_prefetch_*: K3 + K2 per
+// GiB 0.932-0.936 -> 0.910-0.911 ms on 32 KiB streams, 0.900-0.902 -> 0.861-0.864
+// on 64 KiB blocks with the register cap below; uncapped it needs 82 VGPRs, 5
+// waves per SIMD, and is slower: 0.984-0.985)
+#ifndef SNAPPY_K2_PREFETCH
+#define SNAPPY_K2_PREFETCH 1
+#endif
 // measurement only (wrong output): K2 reads no literal bytes from the input, the
 // upper bound of what literals staged by K1r could save K2
 #ifndef SNAPPY_K2_NOLIT
@@ -1867,8 +1875,9 @@ __device__ __forceinline__ void k2_long_literals(uint8_t *w, const uint8_t *__re
 // 1: no register cap (80 VGPRs, 6 waves/SIMD with 128-token passes); capping at
 // 7 or 8 waves spills and measured slower (1.18 / 1.22 against 0.979
 // ms of K3 + K2 per GiB of text)
+// (with the prefetch: 6, i.e. 80 VGPRs, the same occupancy as before it)
 #ifndef SNAPPY_K2_WAVES_PER_EU
-#define SNAPPY_K2_WAVES_PER_EU 1
+#define SNAPPY_K2_WAVES_PER_EU (SNAPPY_K2_PREFETCH ? 6 : 1)
 #endif
 #if SNAPPY_TU_COMPRESS
 __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
@@ -1894,10 +1903,32 @@ __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(cons
         if (hdr_mode == SNAPPY_HDR_EVERY_UNIT) varint_put(L, dst, lane);
         else if (hdr_mode == SNAPPY_HDR_FIRST_UNIT && u == 0) varint_put(header_value, dst, lane);
     }
+#if SNAPPY_K2_PREFETCH
+    // the next pass's token words (and the next segment's record) are loaded one
+    // pass ahead, so their round trip overlaps this pass's literal loads
+    uint32_t kwn[kK2Per];
+    auto load_kw = [&](uint32_t c, uint32_t *k) {
+#pragma unroll
+        for (uint32_t i = 0; i < kK2Per; i++) {
+            const uint32_t t = c + kK2Per * lane + i;
+            k[i] = tok[t < nt ? t : 0u];
+        }
+    };
+    auto load_se = [&](uint32_t sg) {
+        return *reinterpret_cast<const uint2 *>(seg_off + 2 * ((uint64_t)u * segs + (sg * kK2Seg <= nt ? sg : 0u)));
+    };
+    if (blockIdx.y * kK2Seg <= nt) load_kw(blockIdx.y * kK2Seg, kwn);
+    uint2 sen = load_se(blockIdx.y);
+#endif
     for (uint32_t sg = blockIdx.y; sg * kK2Seg <= nt; sg += gridDim.y) {
     // K1r's table: the segment's output offset and the input position where
     // its first literal starts (the end of the previous segment's last token)
+#if SNAPPY_K2_PREFETCH
+    const uint2 se = sen;
+    sen = load_se(sg + gridDim.y);
+#else
     const uint2 se = *reinterpret_cast<const uint2 *>(seg_off + 2 * ((uint64_t)u * segs + sg));
+#endif
     uint32_t o = se.x, carry = se.y;
     for (uint32_t c = sg * kK2Seg; c < (sg + 1) * kK2Seg && c <= nt; c += kK2Pass) {
 
@@ -1907,11 +1938,21 @@ __global__ __launch_bounds__(64, SNAPPY_K2_WAVES_PER_EU) void k2_emit_units(cons
     // the lane's token words in one round trip (a lane past the end re-reads word 0:
     // no branch, so no load waits for the one before it), then the rare escapes
     uint32_t kw[kK2Per];
+#if SNAPPY_K2_PREFETCH
+#pragma unroll
+    for (uint32_t i = 0; i < kK2Per; i++) kw[i] = kwn[i];
+    {
+        uint32_t cn = c + kK2Pass;
+        if (!(cn < (sg + 1) * kK2Seg && cn <= nt)) cn = (sg + gridDim.y) * kK2Seg;
+        if (cn <= nt) load_kw(cn, kwn);
+    }
+#else
 #pragma unroll
     for (uint32_t i = 0; i < kK2Per; i++) {
         const uint32_t t = c + kK2Per * lane + i;
         kw[i] = tok[t < nt ? t : 0u];
     }
+#endif
 #pragma unroll
     for (uint32_t i = 0; i < kK2Per; i++) {
         const uint32_t t = c + kK2Per * lane + i;

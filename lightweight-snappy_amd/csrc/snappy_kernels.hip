@@ -352,6 +352,16 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
     return x - v;
 }
 
+// SNAPPY_K1R_ASM_V16: the lane data carry the in-window predecessor's tag
+// (pdnz), so the hit test selects the candidate's tag and compares it once
+// with the lane's (16-bit field: a lane past the window has bit 24 of its word
+// set and never matches) -- two VALU instead of three.  1 = both kernels, 2 =
+// K1r64 only (A/B, profiles/r05za_*: 64 KiB blocks 15.04-15.08 -> 14.51 ms per
+// GiB, 32 KiB streams 12.89 -> 13.04: the same three instructions fewer measure
+// differently in the two kernels' schedules)
+#ifndef SNAPPY_K1R_ASM_V16
+#define SNAPPY_K1R_ASM_V16 2
+#endif
 template <bool BIG>
 __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
                                          uint32_t hdr_mode, uint64_t header_value,
@@ -620,7 +630,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     uint8_t ent_t = 0;
 #endif
     uint32_t adr = 0, word = 0;               // the lane's table record address and its insert word
-    uint32_t pdnz = 0;
+    uint32_t pdnz = 0;  // the predecessor's tag flag (kV16: its tag)
+    constexpr bool kV16 = SNAPPY_K1R_ASM_V16 == 1 || (SNAPPY_K1R_ASM_V16 == 2 && BIG);
     uint64_t m_win = 0, m_win17 = 0;
     uint64_t m_pdz = 0;  // lanes whose in-window predecessor carries the same tag (pdnz == 0)
     bool lsw = false;  // the lane-space data describe the current window
@@ -663,7 +674,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         pdl1 = _bits ? lane - _pd + 1 - (_pd == 1 ? 1u : 0u) : 0xFFFFFF00u; /* signed: below every lane0 */ \
         pdc = q0 + lane - _pd;                                                                     \
         const uint32_t _hp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - _pd) << 2), (int)hv); \
-        pdnz = _hp == hv ? 0u : 1u; /* 0 iff the predecessor's tag matches */                     \
+        /* 0 iff the predecessor's tag matches; V16: the predecessor's tag */                       \
+        pdnz = kV16 ? (_hp >> 16) & 0xFFu : (_hp == hv ? 0u : 1u);                                 \
         if (SNAPPY_K1R_ASM_V4) m_pdz = __ballot(_hp == hv);                                        \
         /* probe lanes: <= 62 and not past is_block_end (L - p >= 16, 17 at skip 64) */           \
         const int32_t _w16 = (int32_t)(L - 16 - q0), _w17 = (int32_t)(L - 17 - q0);              \
@@ -673,7 +685,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         word = (q0 + lane) | (hv & 0xFF0000u);                                                     \
         if (SNAPPY_K1R_ASM_V6 && !_inw) { /* the asm hit test sees the window mask in the lane data */ \
             word |= 1u << 24;                                                                      \
-            pdnz = 1;                                                                              \
+            if (!kV16) pdnz = 1;                                                                   \
         }                                                                                          \
         lsw = true; /* the caller reads ent */                                                     \
     } while (0)
@@ -857,6 +869,12 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #ifndef SNAPPY_K1R_ASM_V4
 #define SNAPPY_K1R_ASM_V4 0
 #endif
+#define K1R_HIT_V16                                                                                 \
+    "v_cndmask_b32_sdwa %[t1], %[pdc], %[ent], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "             \
+    "src0_sel:DWORD src1_sel:WORD_0\n\t" /* the candidate of every lane */                          \
+    "v_cndmask_b32_e32 %[t0], %[pdnz], %[entt], vcc\n\t" /* and its tag */                          \
+    "v_cmp_eq_u32_sdwa %[hm], %[t0], %[word] src0_sel:DWORD src1_sel:WORD_1\n\t"
+
 #if SNAPPY_K1R_ASM_V4
 #define K1R_V4_HIT                                                                                  \
     "v_cmp_eq_u32_sdwa %[hm], %[entt], %[word] src0_sel:DWORD src1_sel:WORD_1\n\t"                   \
@@ -1008,6 +1026,30 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     "v_mov_b32_e32 %[t4], v3\n\t"                                                                   \
     "s_set_gpr_idx_off\n\t"                                                                         \
     "s_bfe_u32 %[s1], %[c], 0x60002\n\t"
+// SNAPPY_K1R_ASM_V15: the candidate's register pair selected by one indexed
+// v_cndmask (s_set_gpr_idx with SRC0 and SRC1: lanes >= l0 take register R,
+// the others R + 1) instead of two indexed moves and a select (65,536-byte
+// blocks leave the loop at the wrap pair 127 / 0, SNAPPY_K1R64_CAND 1)
+#ifndef SNAPPY_K1R_ASM_V15
+#define SNAPPY_K1R_ASM_V15 1
+#endif
+#if SNAPPY_K1R_ASM_V15 && SNAPPY_K1R64_CAND != 3
+#undef K1R_V10_PAIR
+#define K1R_V10_PAIR                                                                                \
+    "s_bfe_u32 %[s1], %[c], 0x60002\n\t"                                                            \
+    "v_cmp_le_u32_e32 vcc, %[s1], %[lane]\n\t" /* lanes >= l0 take register R */                   \
+    "v_add_u32_e32 %[t1], %[c], %[lane4]\n\t"                                                      \
+    "s_set_gpr_idx_on %[s0], gpr_idx(SRC0,SRC1)\n\t"                                               \
+    "v_cndmask_b32_e32 %[t3], v3, v2, vcc\n\t"                                                     \
+    "s_set_gpr_idx_off\n\t"
+#undef K1R_V5_ROT
+#define K1R_V5_ROT ""
+#undef K1R_V5_SEL
+#define K1R_V5_SEL ""
+#define K1R_V15_CA ""
+#else
+#define K1R_V15_CA K1R_V2_CA
+#endif
 #if SNAPPY_K1R_ASM_V10
 #define K1R_V10_SEL2A "v_mul_i32_i24_e64 %[t0], %[pf], -8\n\t"
 #define K1R_V10_FUNNEL_PA "v_alignbit_b32 %[t2], %[t2], %[t1], %[t0]\n\t"
@@ -1036,6 +1078,106 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     "s_add_i32 %[s3], %[s3], 0x7060504\n\t"
 #define K1R_V11_PERM3 "v_perm_b32 %[t3], %[t3], %[t4], %[s3]\n\t"
 #define K1R_V11_OUTS
+#endif
+// SNAPPY_K1R_ASM_V13: the inserts under an exec mask made by one s_bfm_b64
+// (the round loop runs in uniform control flow with all 64 lanes of the wave
+// live, so it restores exec to all ones; exec cannot be declared clobbered)
+// (lanes lo0 .. f; a missing round's lane0 - 1 .. lane0 - 1 + nk: at most DMAX +
+// 1 lanes, so the 6-bit size never wraps) instead of every lane writing its
+// record or the shared dummy: four VALU (range compare, address select, tag
+// address) for three SALU, and no same-address writes
+#if SNAPPY_K1R_ASM_V16 == 1
+#define K1R_HIT32 K1R_HIT_V16
+#else
+#define K1R_HIT32 K1R_V4_HIT
+#endif
+#if SNAPPY_K1R_ASM_V16 >= 1
+#define K1R_HIT64 K1R_HIT_V16
+#else
+#define K1R_HIT64 K1R_V4_HIT
+#endif
+#ifndef SNAPPY_K1R_ASM_V13
+#define SNAPPY_K1R_ASM_V13 1
+#endif
+// SNAPPY_K1R_ASM_V14 (with V13): a hit round reads the next round's entries
+// only in lanes > f (exec), inside the inserts' exec window
+#ifndef SNAPPY_K1R_ASM_V14
+#define SNAPPY_K1R_ASM_V14 0
+#endif
+#if SNAPPY_K1R_ASM_V13 && SNAPPY_K1R_ASM_V14
+#define K1R_V14_READ_MASK                                                                           \
+    "s_add_u32 %[s2], %[f], 1\n\t"                                                                  \
+    "s_lshl_b64 exec, -1, %[s2]\n\t" /* lanes > f (f <= 62) */                                     \
+    "ds_read_u16 %[ent], %[adr]\n\t"                                                                \
+    "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"
+#define K1R_V14_SKIP_READS 1
+#else
+#define K1R_V14_READ_MASK
+#define K1R_V14_SKIP_READS 0
+#endif
+#if SNAPPY_K1R_ASM_V13
+#define K1R_V13_DUMMY_IN
+#define K1R_V13_HIT_INSERT                                                                          \
+    K1R_V10_SEL2A /* (a VALU result every lane needs: before the exec change) */                   \
+    "s_sub_u32 %[s2], %[f], %[s0]\n\t"                                                              \
+    "s_add_u32 %[s2], %[s2], 1\n\t"                                                                 \
+    "s_bfm_b64 exec, %[s2], %[s0]\n\t" /* lanes lo0 .. f */                                         \
+    "ds_write_b16 %[adr], %[word]\n\t"                                                              \
+    "ds_write_b8_d16_hi %[adrt], %[word] offset:%[tagb]\n\t"                                        \
+    K1R_V14_READ_MASK                                                                               \
+    "s_mov_b64 exec, -1\n\t"
+#define K1R_V13_NOHIT_INSERT                                                                        \
+    "s_add_u32 %[s2], %[skip], %[s0]\n\t"                                                           \
+    "s_add_i32 %[s3], %[s2], -1\n\t"                                                                \
+    "s_add_u32 %[c], %[s0], 1\n\t" /* (c is free on this path) */                                  \
+    "s_bfm_b64 exec, %[c], %[s1]\n\t" /* lanes lane0 - 1 .. lane0 - 1 + nk */                      \
+    "ds_write_b16 %[adr], %[word]\n\t"                                                              \
+    "ds_write_b8_d16_hi %[adrt], %[word] offset:%[tagb]\n\t"                                        \
+    "s_mov_b64 exec, -1\n\t"
+#else
+#define K1R_V13_DUMMY_IN , [dummy] "v"(kDummy)
+#define K1R_V13_HIT_INSERT                                                                          \
+    "v_subrev_u32_e32 %[t4], %[s0], %[lane]\n\t"                                                    \
+    "s_sub_u32 %[s0], %[f], %[s0]\n\t"                                                              \
+    "v_cmp_ge_u32_e32 vcc, %[s0], %[t4]\n\t" /* lanes lo0 .. f insert */                            \
+    K1R_V10_SEL2A                                                                                   \
+    "v_cndmask_b32_e32 %[t4], %[dummy], %[adr], vcc\n\t"                                            \
+    "ds_write_b16 %[t4], %[word]\n\t"                                                               \
+    "v_lshrrev_b32_e32 %[t4], 1, %[t4]\n\t"                                                         \
+    "ds_write_b8_d16_hi %[t4], %[word] offset:%[tagb]\n\t"
+#define K1R_V13_NOHIT_INSERT                                                                        \
+    "v_subrev_u32_e32 %[t4], %[s1], %[lane]\n\t"                                                    \
+    "v_cmp_ge_u32_e32 vcc, %[s0], %[t4]\n\t"                                                        \
+    "s_add_u32 %[s2], %[skip], %[s0]\n\t"                                                           \
+    "s_add_i32 %[s3], %[s2], -1\n\t"                                                                \
+    "v_cndmask_b32_e32 %[t4], %[dummy], %[adr], vcc\n\t"                                            \
+    "ds_write_b16 %[t4], %[word]\n\t"                                                               \
+    "v_lshrrev_b32_e32 %[t4], 1, %[t4]\n\t"                                                         \
+    "ds_write_b8_d16_hi %[t4], %[word] offset:%[tagb]\n\t"
+#endif
+// SNAPPY_K1R_ASM_V12: a hit round's entry reads only for lanes > f (the next
+// round starts at f + len >= f + 4); lanes <= f read the dummy record (one
+// address: a broadcast, no bank conflicts -- K1r's LDS spent 38 % of its active
+// cycles in bank conflicts, profiles/r05v_*).  The SEL3 scalar instructions fill
+// the compare's two wait states before the select reads vcc
+#ifndef SNAPPY_K1R_ASM_V12
+#define SNAPPY_K1R_ASM_V12 0
+#endif
+#if SNAPPY_K1R_ASM_V12
+#define K1R_V12_READS                                                                               \
+    "v_cmp_lt_u32_e32 vcc, %[f], %[lane]\n\t"                                                      \
+    K1R_V11_SEL3                                                                                    \
+    "v_cndmask_b32_e32 %[t4], %[dummy], %[adr], vcc\n\t"                                            \
+    "ds_read_u16 %[ent], %[t4]\n\t"                                                                \
+    "v_lshrrev_b32_e32 %[t4], 1, %[t4]\n\t"                                                        \
+    "ds_read_u8 %[entt], %[t4] offset:%[tagb]\n\t"
+#elif K1R_V14_SKIP_READS
+#define K1R_V12_READS K1R_V11_SEL3
+#else
+#define K1R_V12_READS                                                                               \
+    "ds_read_u16 %[ent], %[adr]\n\t"                                                               \
+    "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"                                               \
+    K1R_V11_SEL3
 #endif
 #if SNAPPY_K1R_ASM_V7
 #define K1R_V7_P ""
@@ -1139,7 +1281,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     "s_cbranch_scc1 L%=_top\n\t"                                                                    \
     "s_branch L%=_x2\n"
 #endif
-#define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, CAND, SEGHI, WRAP)                                    \
+#define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, CAND, SEGHI, WRAP, HIT)                                    \
     do {                                                                                            \
         uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4, _t5, _t6;                 \
         (void)_t5;                                                                                  \
@@ -1154,7 +1296,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "v_cmp_gt_i32_e32 vcc, %[lane0], %[pdl1]\n\t" /* vcc = not in-round */                  \
             K1R_V6_MWIN_HIT                                                                         \
             "s_waitcnt lgkmcnt(0)\n\t"                                                              \
-            K1R_V4_HIT                                                                              \
+            HIT                                                                                     \
             "s_and_b64 %[hm], %[hm], %[valid]\n\t"                                                  \
             K1R_V2_HITBR                                                                            \
             "s_ff1_i32_b64 %[f], %[hm]\n\t"                                                         \
@@ -1167,24 +1309,15 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             K1R_V10_PAIR                                                                            \
             WRAP                                                                                    \
             K1R_V5_ROT                                                                              \
-            K1R_V2_CA                                                                               \
+            K1R_V15_CA                                                                              \
             K1R_V5_SEL                                                                              \
             "ds_bpermute_b32 %[t3], %[t1], %[t3]\n\t" /* ca: dwords at c */                         \
             K1R_V6_DRAIN /* the previous round's token, during the gathers */                      \
             "s_add_u32 %[pend], %[pend], %[dkn]\n\t"                                                \
             K1R_V5_LO0                                                                              \
-            "v_subrev_u32_e32 %[t4], %[s0], %[lane]\n\t"                                            \
-            "s_sub_u32 %[s0], %[f], %[s0]\n\t"                                                      \
-            "v_cmp_ge_u32_e32 vcc, %[s0], %[t4]\n\t" /* lanes lo0 .. f insert */                    \
-            K1R_V10_SEL2A                                                                           \
-            "v_cndmask_b32_e32 %[t4], %[dummy], %[adr], vcc\n\t"                                    \
-            "ds_write_b16 %[t4], %[word]\n\t"                                                       \
-            "v_lshrrev_b32_e32 %[t4], 1, %[t4]\n\t"                                                 \
-            "ds_write_b8_d16_hi %[t4], %[word] offset:%[tagb]\n\t"                                  \
-            "ds_read_u16 %[ent], %[adr]\n\t"                                                        \
-            "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"                                        \
+            K1R_V13_HIT_INSERT                                                                      \
+            K1R_V12_READS                                                                           \
             K1R_V6_SEL2B                                                                            \
-            K1R_V11_SEL3                                                                            \
             "s_waitcnt lgkmcnt(2)\n\t" /* pa, ca and the inserts; the entry reads stay in flight */ \
             "v_mov_b32_dpp %[t1], %[t2] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
             "v_mov_b32_dpp %[t4], %[t3] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
@@ -1202,14 +1335,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "s_mov_b32 %[dkn], 0\n\t"                                                               \
             K1R_V9_DKZERO                                                                           \
             "s_add_i32 %[s1], %[lane0], -1\n\t"                                                     \
-            "v_subrev_u32_e32 %[t4], %[s1], %[lane]\n\t"                                            \
-            "v_cmp_ge_u32_e32 vcc, %[s0], %[t4]\n\t"                                                \
-            "s_add_u32 %[s2], %[skip], %[s0]\n\t"                                                   \
-            "s_add_i32 %[s3], %[s2], -1\n\t"                                                        \
-            "v_cndmask_b32_e32 %[t4], %[dummy], %[adr], vcc\n\t"                                    \
-            "ds_write_b16 %[t4], %[word]\n\t"                                                       \
-            "v_lshrrev_b32_e32 %[t4], 1, %[t4]\n\t"                                                 \
-            "ds_write_b8_d16_hi %[t4], %[word] offset:%[tagb]\n\t"                                  \
+            K1R_V13_NOHIT_INSERT                                                                    \
             "ds_read_u16 %[ent], %[adr]\n\t"                                                        \
             "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"                                        \
             "s_lshr_b32 %[s3], %[s3], 5\n\t" /* the last probe steps by 2 at skip 64 */             \
@@ -1244,7 +1370,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
               [pdz] "s"(m_pdz),                                                                     \
               [dv] "v"(dv),                                                                         \
               [pdl1] "v"(pdl1), [pdc] "v"(pdc), [pdnz] "v"(pdnz), [adr] "v"(adr), [adrt] "v"(adr >> 1), \
-              [word] "v"(word), [lane] "v"(lane), [lane4] "v"(lane << 2), [dummy] "v"(kDummy),         \
+              [word] "v"(word), [lane] "v"(lane), [lane4] "v"(lane << 2) K1R_V13_DUMMY_IN,         \
               [skipmax] "i"(64 - DMAX), [dmask] "i"((1u << DMAX) - 1), [lsmax] "i"(64 - SNAPPY_K1R_LSMIN), \
               [l0max] "i"(62 - SNAPPY_K1R_RMIN), [tagb] "i"(kTagBase), "{v[2:33]}"(g0), "{v[34:65]}"(g1), \
               "{v[66:97]}"(g2), "{v[98:129]}"(g3)                                                      \
@@ -1337,9 +1463,10 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     RSTAMP(ra0);
 #endif
                     if constexpr (BIG)
-                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND64, K1R_SEGHI64(seg_hi), K1R_WRAP64);
+                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND64, K1R_SEGHI64(seg_hi), K1R_WRAP64,
+                                            K1R_HIT64);
                     else
-                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND32, "i"(0), "");
+                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND32, "i"(0), "", K1R_HIT32);
 #ifdef SNAPPY_K1R_RSTAMPS
                     RSTAMP(ra1);
                     rs_asm += ra1 - ra0;
@@ -1404,7 +1531,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 // lane l > lane0 takes the in-round candidate when its nearest same-hash lane is >= lane0 - 1;
                 // the hit test selects per lane (VALU) so one ballot carries it to SALU
                 const bool inr = (int32_t)pdl1 >= (int32_t)lane0;
-                const uint32_t hitnz = inr ? pdnz : ((ent_t ^ (word >> 16)) & 0xFFu);
+                const uint32_t hitnz = kV16 ? (inr ? pdnz : (uint32_t)ent_t) ^ ((word >> 16) & 0xFFu)
+                                                          : (inr ? pdnz : ((ent_t ^ (word >> 16)) & 0xFFu));
                 const uint64_t hm = __ballot(hitnz == 0) & valid;
                 const uint32_t candv = inr ? pdc : ent;
                 const uint32_t f = (uint32_t)__builtin_ctzll(hm);

@@ -1192,6 +1192,21 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #else
 #define K1R_V7_P "s_add_u32 %[p], %[pf], %[s0]\n\t"
 #endif
+// SNAPPY_K1R_ASM_V17 (with V7): the prefix length from the first differing
+// dword's xor read back and finished in SALU (s_flbit, s_lshr, s_lshl2_add)
+// instead of ffbh / bfe / lshl_or on every lane
+#ifndef SNAPPY_K1R_ASM_V17
+#define SNAPPY_K1R_ASM_V17 0
+#endif
+#if SNAPPY_K1R_ASM_V7 && SNAPPY_K1R_ASM_V17
+#undef K1R_V3_LEN
+#undef K1R_V3_DIV
+#define K1R_V3_LEN "v_xor_b32_e32 %[t2], %[t2], %[t3]\n\t"
+#define K1R_V3_DIV                                                                                  \
+    "s_flbit_i32_b32 %[s0], %[s0]\n\t"                                                              \
+    "s_lshr_b32 %[s0], %[s0], 3\n\t"                                                                \
+    "s_lshl2_add_u32 %[s0], %[s1], %[s0]\n\t" /* 4 k + the equal bytes of dword k */
+#endif
 #if SNAPPY_K1R_ASM_V2 && SNAPPY_K1R_ASM_V6
 #define K1R_V2_TAIL                                                                                 \
     "s_ff1_i32_b32 %[s1], vcc_lo\n\t"                                                               \

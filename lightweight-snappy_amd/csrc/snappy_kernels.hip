@@ -3123,9 +3123,15 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 s.pend = o < op_end;
                 uint32_t t = o + f_x;
                 s.far = s.pend && !s.lit && t < lo;
+#if SNAPPY_K4_PASS_PIPE == 2
+                // every lane loads (a lane that is not far reads dst[0]: one line), so
+                // the load is straight-line code whose wait the compiler can count
+                s.fv = dst[s.far ? t : 0u];
+#else
                 asm volatile("" : "=v"(s.fv));  // (no initial value: read only where far)
 #ifndef SNAPPY_K4_NOFAR
                 if (s.far) s.fv = dst[t];
+#endif
 #endif
                 const uint32_t a2 = t - 768;
                 s.lb = wb[__builtin_elementwise_min(__builtin_elementwise_min(t, a2), 783u)];
@@ -3138,7 +3144,45 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 s.t = t;
             };
             PassA cur, nxt;
+#if SNAPPY_K4_PASS_PIPE == 2
+            // ping-pong (no register copies of in-flight loads at the loop latch)
+            auto stage_b = [&](uint32_t P, const PassA &c) {
+                const uint32_t o = P + lane;
+                const int32_t tin = (c.pend && !c.lit && !c.far) ? (int32_t)c.t : -1;
+                const uint8_t rv = ob[c.t & M];
+                const uint8_t lr = c.lit ? (uint8_t)c.lb : rv;
+                uint32_t val = c.far ? c.fv : (uint32_t)lr;
+                if (__builtin_expect(__ballot(tin >= (int32_t)P) != 0, 0)) {
+                    uint32_t rt = tin >= (int32_t)P ? c.t - P : lane;
+                    for (;;) {
+                        const uint32_t r2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rt << 2), (int)rt);
+                        if (!__ballot(r2 != rt)) break;
+                        rt = r2;
+                    }
+                    val = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rt << 2), (int)val);
+                }
+                ob[c.pend ? (o & M) : kK4Ring] = (uint8_t)val;
+            };
+            PassA sa, sb;
+            stage_a(op, 0, sa);
+            for (uint32_t P = op, i = 0;;) {
+                const bool m1 = P + 64 < op_end;
+                if (m1) stage_a(P + 64, i + 1, sb);
+                stage_b(P, sa);
+                if (!m1) break;
+                P += 64;
+                i++;
+                const bool m2 = P + 64 < op_end;
+                if (m2) stage_a(P + 64, i + 1, sa);
+                stage_b(P, sb);
+                if (!m2) break;
+                P += 64;
+                i++;
+            }
+            if (false)
+#else
             stage_a(op, 0, cur);
+#endif
             for (uint32_t P = op, i = 0; P < op_end; P += 64, i++) {
                 if (P + 64 < op_end) stage_a(P + 64, i + 1, nxt);
                 const uint32_t o = P + lane;

@@ -1155,6 +1155,40 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     "v_lshrrev_b32_e32 %[t4], 1, %[t4]\n\t"                                                         \
     "ds_write_b8_d16_hi %[t4], %[word] offset:%[tagb]\n\t"
 #endif
+// SNAPPY_K1R_ASM_V18 (with V13): a hit round's inserts and entry reads issued
+// after the wait for the two gathers (and behind the funnels), so that wait no
+// longer covers the insert writes; they complete during the verification (A/B,
+// outputs identical, profiles/r05zf_*: 32 KiB streams 12.89 -> 12.69 ms per GiB,
+// 64 KiB blocks 14.50 -> 14.23-14.28)
+#ifndef SNAPPY_K1R_ASM_V18
+#define SNAPPY_K1R_ASM_V18 1
+#endif
+#if SNAPPY_K1R_ASM_V18 && SNAPPY_K1R_ASM_V13 && !SNAPPY_K1R_ASM_V14 && !SNAPPY_K1R_ASM_V12
+#define K1R_V18_PRE                                                                                 \
+    K1R_V10_SEL2A                                                                                   \
+    "s_sub_u32 %[s2], %[f], %[s0]\n\t"                                                              \
+    "s_add_u32 %[s2], %[s2], 1\n\t"                                                                 \
+    K1R_V11_SEL3
+#define K1R_V18_WAIT "s_waitcnt lgkmcnt(0)\n\t" /* pa and ca */
+#define K1R_V18_POST                                                                                \
+    "s_bfm_b64 exec, %[s2], %[s0]\n\t" /* lanes lo0 .. f insert */                                  \
+    "ds_write_b16 %[adr], %[word]\n\t"                                                              \
+    "ds_write_b8_d16_hi %[adrt], %[word] offset:%[tagb]\n\t"                                        \
+    "s_mov_b64 exec, -1\n\t"                                                                        \
+    "ds_read_u16 %[ent], %[adr]\n\t"                                                                \
+    "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"
+// (placing them after the match length's read-back instead, with lo0 kept in
+// s3: 32 KiB streams -1.3 %, 64 KiB blocks +1.8 % against this placement;
+// its s3 copy alone cost 0.6 %: profiles/r05zg_*)
+#define K1R_V18_MID
+#define K1R_V18_X4
+#else
+#define K1R_V18_PRE K1R_V13_HIT_INSERT K1R_V12_READS
+#define K1R_V18_WAIT "s_waitcnt lgkmcnt(2)\n\t" /* pa, ca and the inserts; the entry reads stay in flight */
+#define K1R_V18_POST
+#define K1R_V18_MID
+#define K1R_V18_X4
+#endif
 // SNAPPY_K1R_ASM_V12: a hit round's entry reads only for lanes > f (the next
 // round starts at f + len >= f + 4); lanes <= f read the dummy record (one
 // address: a broadcast, no bank conflicts -- K1r's LDS spent 38 % of its active
@@ -1214,6 +1248,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     "s_cbranch_scc1 L%=_x4\n\t"                                                                     \
     "v_readlane_b32 %[s0], %[t2], %[s1]\n\t"                                                        \
     K1R_V3_DIV                                                                                      \
+    K1R_V18_MID                                                                                     \
     "s_cmp_lt_u32 %[s0], 4\n\t" /* (pf <= L - 16: the clamp below never makes it < 4) */            \
     "s_cbranch_scc1 L%=_x5\n\t"                                                                     \
     "s_add_u32 %[lane0], %[f], %[s0]\n\t"                                                           \
@@ -1330,14 +1365,14 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             K1R_V6_DRAIN /* the previous round's token, during the gathers */                      \
             "s_add_u32 %[pend], %[pend], %[dkn]\n\t"                                                \
             K1R_V5_LO0                                                                              \
-            K1R_V13_HIT_INSERT                                                                      \
-            K1R_V12_READS                                                                           \
+            K1R_V18_PRE                                                                             \
             K1R_V6_SEL2B                                                                            \
-            "s_waitcnt lgkmcnt(2)\n\t" /* pa, ca and the inserts; the entry reads stay in flight */ \
+            K1R_V18_WAIT                                                                            \
             "v_mov_b32_dpp %[t1], %[t2] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
             "v_mov_b32_dpp %[t4], %[t3] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
             K1R_V10_FUNNEL_PA                                                                       \
             K1R_V11_PERM3                                                                           \
+            K1R_V18_POST                                                                            \
             "v_cmp_ne_u32_e32 vcc, %[t2], %[t3]\n\t"                                                \
             K1R_V3_LEN                                                                              \
             K1R_V2_TAIL                                                                             \
@@ -1368,7 +1403,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "L%=_x3:\n\ts_mov_b32 %[code], 3\n\ts_branch L%=_end\n"                                 \
             "L%=_x1:\n\ts_mov_b32 %[code], 1\n\ts_branch L%=_end\n"                                 \
             "L%=_x2:\n\ts_mov_b32 %[code], 2\n\ts_branch L%=_end\n"                                 \
-            "L%=_x4:\n\ts_mov_b32 %[code], 4\n\ts_branch L%=_end\n"                                 \
+            "L%=_x4:\n\t" K1R_V18_X4 "s_mov_b32 %[code], 4\n\ts_branch L%=_end\n"                   \
             "L%=_x5:\n\ts_mov_b32 %[code], 5\n"                                                     \
             "L%=_end:\n\t"                                                                          \
             K1R_V8_SKIPFIX                                                                          \

@@ -797,6 +797,30 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #define SNAPPY_K1R_ASM_BIG 1
 #endif
 #define K1R_CAND32 "s_lshr_b32 %[s0], %[c], 8\n\t"
+// SNAPPY_K1R_ASM_V19 (65,536-byte blocks, CAND 1): a candidate whose segment has
+// left the register ring is gathered from the input in the loop (one
+// global_load_dword per lane, waited for at once: the candidate lies >= 32 KiB
+// before the window, so its 256 bytes are inside the block) instead of leaving
+// for the C++ round (A/B, outputs identical, profiles/r05zi_*: 64 KiB text
+// blocks 14.23-14.27 -> 14.09 ms per GiB, random 3.98-4.01 -> 4.02-4.04)
+#ifndef SNAPPY_K1R_ASM_V19
+#define SNAPPY_K1R_ASM_V19 1
+#endif
+#if SNAPPY_K1R_ASM_V19
+#define K1R_V19_TARGET "far"
+#define K1R_V19_FAR                                                                                 \
+    "L%=_far:\n\t"                                                                                   \
+    "s_and_b32 %[s1], %[c], -4\n\t"                                                                 \
+    "v_add_u32_e32 %[t1], %[s1], %[lane4]\n\t"                                                      \
+    "global_load_dword %[t3], %[t1], %[srcb]\n\t"                                                   \
+    "s_mov_b32 %[s1], 0x10203\n\t"                                                                  \
+    "s_waitcnt vmcnt(0)\n\t"                                                                        \
+    "v_perm_b32 %[t3], %[t3], %[t3], %[s1]\n\t" /* big-endian, as the ring registers */             \
+    "s_branch L%=_farret\n"
+#else
+#define K1R_V19_TARGET "x3"
+#define K1R_V19_FAR
+#endif
 // SNAPPY_K1R64_CAND (A/B, 1 GiB of 64 KiB text blocks, outputs identical,
 // profiles/r05b_ab_*, r05c_ab_*): 0 = the two tests as shifts and compares of
 // the segment index (18.70 ms); 1 = the residency test as one compare of the
@@ -821,7 +845,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #elif SNAPPY_K1R64_CAND == 1
 #define K1R_CAND64                                                                                  \
     "s_cmp_lt_u32 %[c], %[seghi]\n\t"                                                              \
-    "s_cbranch_scc1 L%=_x3\n\t"                                                                    \
+    "s_cbranch_scc1 L%=_" K1R_V19_TARGET "\n\t"                                                     \
     "s_bfe_u32 %[s0], %[c], 0x70008\n\t"                                                           \
     "s_cmp_eq_u32 %[s0], 127\n\t"                                                                  \
     "s_cbranch_scc1 L%=_x3\n\t"
@@ -1362,6 +1386,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             K1R_V15_CA                                                                              \
             K1R_V5_SEL                                                                              \
             "ds_bpermute_b32 %[t3], %[t1], %[t3]\n\t" /* ca: dwords at c */                         \
+            "L%=_farret:\n\t"                                                                       \
             K1R_V6_DRAIN /* the previous round's token, during the gathers */                      \
             "s_add_u32 %[pend], %[pend], %[dkn]\n\t"                                                \
             K1R_V5_LO0                                                                              \
@@ -1404,6 +1429,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "L%=_x1:\n\ts_mov_b32 %[code], 1\n\ts_branch L%=_end\n"                                 \
             "L%=_x2:\n\ts_mov_b32 %[code], 2\n\ts_branch L%=_end\n"                                 \
             "L%=_x4:\n\t" K1R_V18_X4 "s_mov_b32 %[code], 4\n\ts_branch L%=_end\n"                   \
+            K1R_V19_FAR                                                                             \
             "L%=_x5:\n\ts_mov_b32 %[code], 5\n"                                                     \
             "L%=_end:\n\t"                                                                          \
             K1R_V8_SKIPFIX                                                                          \
@@ -1420,7 +1446,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
               [pdz] "s"(m_pdz),                                                                     \
               [dv] "v"(dv),                                                                         \
               [pdl1] "v"(pdl1), [pdc] "v"(pdc), [pdnz] "v"(pdnz), [adr] "v"(adr), [adrt] "v"(adr >> 1), \
-              [word] "v"(word), [lane] "v"(lane), [lane4] "v"(lane << 2) K1R_V13_DUMMY_IN,         \
+              [word] "v"(word), [lane] "v"(lane), [lane4] "v"(lane << 2) K1R_V13_DUMMY_IN, [srcb] "s"(src),         \
               [skipmax] "i"(64 - DMAX), [dmask] "i"((1u << DMAX) - 1), [lsmax] "i"(64 - SNAPPY_K1R_LSMIN), \
               [l0max] "i"(62 - SNAPPY_K1R_RMIN), [tagb] "i"(kTagBase), "{v[2:33]}"(g0), "{v[34:65]}"(g1), \
               "{v[66:97]}"(g2), "{v[98:129]}"(g3)                                                      \

@@ -635,6 +635,14 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     uint64_t m_win = 0, m_win17 = 0;
     uint64_t m_pdz = 0;  // lanes whose in-window predecessor carries the same tag (pdnz == 0)
     bool lsw = false;  // the lane-space data describe the current window
+// SNAPPY_K1R_WIN_ALIGN: a window's per-lane BE32 by v_alignbit from (p - 1) / 4
+// (as the round loop's pa funnel, V6) instead of v_perm with a per-lane
+// selector from a 32-bit multiply; 32 KiB units only (A/B, outputs identical,
+// profiles/r05zj_*: 32 KiB streams 12.64 -> 12.55-12.57 ms per GiB, but 64 KiB
+// blocks 14.06 -> 14.41 in K1r64's schedule)
+#ifndef SNAPPY_K1R_WIN_ALIGN
+#define SNAPPY_K1R_WIN_ALIGN 1
+#endif
 #define WINDOW_AT(qq)                                                                              \
     do {                                                                                           \
         q0 = (qq);                                                                                 \
@@ -646,10 +654,20 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             REG_PAIR(d0 >> 6, _r0, _r1);                                                           \
             dv = lane >= dr ? _r0 : _r1;                                                           \
         }                                                                                          \
-        const uint32_t _k = d0 + (((q0 & 3) + lane) >> 2); /* rotated by dr = d0 % 64 */         \
-        const uint32_t _a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_k << 2), (int)dv);       \
-        const uint32_t _b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_k + 1) << 2), (int)dv); \
-        bv = funnel_bytes(_a, _b, perm_sel((q0 + lane) & 3));                                     \
+        if (SNAPPY_K1R_WIN_ALIGN && !BIG) {                                                        \
+            /* the dwords from (p - 1) / 4 funnelled by v_alignbit with the lane's */              \
+            /* shift -8 p (bits 4:0; 0 takes the second dword, the one at p) */                    \
+            const uint32_t _p = q0 + lane;                                                          \
+            const uint32_t _k = (_p - 1) >> 2; /* rotated by dr = d0 % 64 */                       \
+            const uint32_t _a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_k << 2), (int)dv);   \
+            const uint32_t _b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_k + 1) << 2), (int)dv); \
+            bv = __builtin_amdgcn_alignbit(_a, _b, 0u - (_p << 3));                                  \
+        } else {                                                                                   \
+            const uint32_t _k = d0 + (((q0 & 3) + lane) >> 2); /* rotated by dr = d0 % 64 */     \
+            const uint32_t _a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(_k << 2), (int)dv);   \
+            const uint32_t _b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_k + 1) << 2), (int)dv); \
+            bv = funnel_bytes(_a, _b, perm_sel((q0 + lane) & 3));                                 \
+        }                                                                                          \
         if (SNAPPY_K1R_TAG1) {                                                                     \
             const uint32_t _pr = bv * kMul;                                                        \
             hv = (_pr >> shift) | (__builtin_amdgcn_ubfe(_pr, shift - 8, 8) << 16);                \

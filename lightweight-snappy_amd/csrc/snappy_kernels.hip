@@ -1128,6 +1128,27 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 // 1 lanes, so the 6-bit size never wraps) instead of every lane writing its
 // record or the shared dummy: four VALU (range compare, address select, tag
 // address) for three SALU, and no same-address writes
+// SNAPPY_K1R_ASM_V20 (32 KiB units): the pa gather address as f + lq, lq = q0 -
+// 1 + 4 lane per asm entry, so the scalar pf = q0 + f leaves the gather's chain
+#ifndef SNAPPY_K1R_ASM_V20
+#define SNAPPY_K1R_ASM_V20 0
+#endif
+#define K1R_PA64                                                                                    \
+    "v_readlane_b32 %[c], %[t1], %[f]\n\t"                                                          \
+    "s_add_u32 %[pf], %[q0], %[f]\n\t" K1R_V2_PA                                                    \
+    "ds_bpermute_b32 %[t2], %[t2], %[dv]\n\t" /* pa: dwords at pf */
+#if SNAPPY_K1R_ASM_V20 && SNAPPY_K1R_ASM_V6
+// (and the pa gather issued before the candidate's read-back)
+#define K1R_PA32                                                                                    \
+    "v_add_u32_e32 %[t2], %[f], %[lq]\n\t" /* dwords from (pf - 1) / 4: see V6 */                  \
+    "ds_bpermute_b32 %[t2], %[t2], %[dv]\n\t" /* pa: dwords at pf */                                \
+    "v_readlane_b32 %[c], %[t1], %[f]\n\t"                                                          \
+    "s_add_u32 %[pf], %[q0], %[f]\n\t"
+#define K1R_LQ32 (lane << 2) + q0 - 1
+#else
+#define K1R_PA32 K1R_PA64
+#define K1R_LQ32 lane << 2
+#endif
 #if SNAPPY_K1R_ASM_V16 == 1
 #define K1R_HIT32 K1R_HIT_V16
 #else
@@ -1373,7 +1394,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     "s_cbranch_scc1 L%=_top\n\t"                                                                    \
     "s_branch L%=_x2\n"
 #endif
-#define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, CAND, SEGHI, WRAP, HIT)                                    \
+#define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, CAND, SEGHI, WRAP, HIT, PA, LQ)                                    \
     do {                                                                                            \
         uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4, _t5, _t6;                 \
         (void)_t5;                                                                                  \
@@ -1392,10 +1413,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "s_and_b64 %[hm], %[hm], %[valid]\n\t"                                                  \
             K1R_V2_HITBR                                                                            \
             "s_ff1_i32_b64 %[f], %[hm]\n\t"                                                         \
-            "v_readlane_b32 %[c], %[t1], %[f]\n\t"                                                  \
-            "s_add_u32 %[pf], %[q0], %[f]\n\t"                                                      \
-            K1R_V2_PA                                                                               \
-            "ds_bpermute_b32 %[t2], %[t2], %[dv]\n\t" /* pa: dwords at pf */                        \
+            PA                                                                                      \
             K1R_V2_CMASK                                                                            \
             CAND                                                                                    \
             K1R_V10_PAIR                                                                            \
@@ -1464,7 +1482,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
               [pdz] "s"(m_pdz),                                                                     \
               [dv] "v"(dv),                                                                         \
               [pdl1] "v"(pdl1), [pdc] "v"(pdc), [pdnz] "v"(pdnz), [adr] "v"(adr), [adrt] "v"(adr >> 1), \
-              [word] "v"(word), [lane] "v"(lane), [lane4] "v"(lane << 2) K1R_V13_DUMMY_IN, [srcb] "s"(src),         \
+              [word] "v"(word), [lane] "v"(lane), [lane4] "v"(lane << 2) K1R_V13_DUMMY_IN, [srcb] "s"(src), [lq] "v"(LQ),         \
               [skipmax] "i"(64 - DMAX), [dmask] "i"((1u << DMAX) - 1), [lsmax] "i"(64 - SNAPPY_K1R_LSMIN), \
               [l0max] "i"(62 - SNAPPY_K1R_RMIN), [tagb] "i"(kTagBase), "{v[2:33]}"(g0), "{v[34:65]}"(g1), \
               "{v[66:97]}"(g2), "{v[98:129]}"(g3)                                                      \
@@ -1558,9 +1576,10 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #endif
                     if constexpr (BIG)
                         K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND64, K1R_SEGHI64(seg_hi), K1R_WRAP64,
-                                            K1R_HIT64);
+                                            K1R_HIT64, K1R_PA64, lane << 2);
                     else
-                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND32, "i"(0), "", K1R_HIT32);
+                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND32, "i"(0), "", K1R_HIT32, K1R_PA32,
+                                            K1R_LQ32);
 #ifdef SNAPPY_K1R_RSTAMPS
                     RSTAMP(ra1);
                     rs_asm += ra1 - ra0;

@@ -2457,7 +2457,15 @@ __device__ __forceinline__ void k4_flush(const uint8_t *ob, uint32_t M, uint8_t 
 // source dwords: an aligned dword holding a byte of the literal never crosses
 // a page the literal does not touch), and its last min(kl, ring) bytes into the
 // ring (later copies read only that far back from the ring; further back, HBM)
-__device__ __noinline__ void k4_literal_hbm(const uint8_t *lsrc, uint32_t kl, uint32_t kop, uint8_t *ob, uint32_t M,
+#ifndef SNAPPY_K4_LIT_INLINE
+#define SNAPPY_K4_LIT_INLINE 0
+#endif
+#if SNAPPY_K4_LIT_INLINE
+#define K4_LIT_ATTR __forceinline__
+#else
+#define K4_LIT_ATTR __noinline__
+#endif
+__device__ K4_LIT_ATTR void k4_literal_hbm(const uint8_t *lsrc, uint32_t kl, uint32_t kop, uint8_t *ob, uint32_t M,
                                                uint8_t *dst, uint32_t lane)
 {
     uint8_t *const d = dst + kop;

@@ -633,7 +633,6 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     uint32_t pdnz = 0;  // the predecessor's tag flag (kV16: its tag)
     constexpr bool kV16 = SNAPPY_K1R_ASM_V16 == 1 || (SNAPPY_K1R_ASM_V16 == 2 && BIG);
     uint64_t m_win = 0, m_win17 = 0;
-    uint64_t m_pdz = 0;  // lanes whose in-window predecessor carries the same tag (pdnz == 0)
     bool lsw = false;  // the lane-space data describe the current window
 // SNAPPY_K1R_WIN_ALIGN: a window's per-lane BE32 by v_alignbit from (p - 1) / 4
 // (as the round loop's pa funnel, V6) instead of v_perm with a per-lane
@@ -694,14 +693,13 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         const uint32_t _hp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - _pd) << 2), (int)hv); \
         /* 0 iff the predecessor's tag matches; V16: the predecessor's tag */                       \
         pdnz = kV16 ? (_hp >> 16) & 0xFFu : (_hp == hv ? 0u : 1u);                                 \
-        if (SNAPPY_K1R_ASM_V4) m_pdz = __ballot(_hp == hv);                                        \
         /* probe lanes: <= 62 and not past is_block_end (L - p >= 16, 17 at skip 64) */           \
         const int32_t _w16 = (int32_t)(L - 16 - q0), _w17 = (int32_t)(L - 17 - q0);              \
         const bool _inw = (int32_t)lane <= _w16 && lane <= 62;                                     \
         m_win = __ballot(_inw);                                                                    \
         m_win17 = __ballot((int32_t)lane <= _w17 && lane <= 62);                                   \
         word = (q0 + lane) | (hv & 0xFF0000u);                                                     \
-        if (SNAPPY_K1R_ASM_V6 && !_inw) { /* the asm hit test sees the window mask in the lane data */ \
+        if (!_inw) { /* the asm hit test sees the window mask in the lane data */                  \
             word |= 1u << 24;                                                                      \
             if (!kV16) pdnz = 1;                                                                   \
         }                                                                                          \
@@ -807,599 +805,79 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #define K1R_ASM_ROUNDS 0
 #endif
 #if K1R_ASM_ROUNDS
-// the candidate's register pair: 32 KiB units read registers c / 256, c / 256 + 1;
-// 65,536-byte blocks read ring registers (c / 256) mod 128 and the next, and leave
-// the loop for the C++ round (code 3) when the candidate's segment has left the
-// ring (a gather from global memory) or is the wrap pair 127 / 0
-#ifndef SNAPPY_K1R_ASM_BIG
-#define SNAPPY_K1R_ASM_BIG 1
-#endif
+// Round 5 took the loop through A/B variants V2-V20 (1 GiB of 32 KiB streams and
+// of 64 KiB blocks each, outputs checked identical; DESIGN.md 4.2 lists them, the
+// logs are profiles/r05e_* .. r05zk_*).  What stayed, in the order the round runs:
+//  * the hit test: the candidate of every lane (in-window predecessor or table
+//    entry) and its tag compared in one SDWA compare (K1r64: the lane data carry
+//    the predecessor's tag, V16; K1r keeps the tag-difference select, which
+//    measured faster in its schedule); a lane past the window has bit 24 of its
+//    word set, so it never matches (V6); the hit branch on the SCC of the s_and
+//    that makes the hit mask (V2)
+//  * pa: the dwords at pf gathered from (pf - 1) / 4 and funnelled by v_alignbit
+//    with the shift -8 pf from v_mul_i32_i24 (bits 4:0; 0 takes the second
+//    dword, the one at pf) (V6, V10)
+//  * ca: the candidate's register pair R, R + 1 selected by one v_cndmask with
+//    s_set_gpr_idx on SRC0 and SRC1 (lanes >= l0 take R; V15); K1r64 reads ring
+//    registers (c / 256) mod 128: a candidate whose segment left the ring is
+//    gathered from the input (global_load_dword, byte-swapped to the ring's
+//    big-endian dwords; V19), the wrap pair 127 / 0 leaves for the C++ round
+//  * the previous round's token drained into tka / tkb during the gathers, its
+//    first word by one s_pack_ll_b32_b16 (V9); lo0 = lane0 - (lane0 < f) by
+//    s_subb (V5)
+//  * the wait for pa and ca alone; the inserts of lanes lo0 .. f under an exec
+//    mask from one s_bfm_b64 (at most DMAX + 1 lanes, so the 6-bit size never
+//    wraps; no dummy-record writes: V13) and the next round's entry reads issued
+//    after it, behind the funnels (V18)
+//  * the prefix length per lane as (clz(xor) >> 3) | 4 lane, read back from the
+//    first differing dword (V3, V7); skip is not reset by a hit round (a pending
+//    token implies skip 32, V8); the clamp to the block end only on the exit path
+// The loop runs in uniform control flow with all 64 lanes live, so it restores
+// exec to all ones after each masked insert (exec cannot be declared clobbered).
 #define K1R_CAND32 "s_lshr_b32 %[s0], %[c], 8\n\t"
-// SNAPPY_K1R_ASM_V19 (65,536-byte blocks, CAND 1): a candidate whose segment has
-// left the register ring is gathered from the input in the loop (one
-// global_load_dword per lane, waited for at once: the candidate lies >= 32 KiB
-// before the window, so its 256 bytes are inside the block) instead of leaving
-// for the C++ round (A/B, outputs identical, profiles/r05zi_*: 64 KiB text
-// blocks 14.23-14.27 -> 14.09 ms per GiB, random 3.98-4.01 -> 4.02-4.04)
-#ifndef SNAPPY_K1R_ASM_V19
-#define SNAPPY_K1R_ASM_V19 1
-#endif
-#if SNAPPY_K1R_ASM_V19
-#define K1R_V19_TARGET "far"
-#define K1R_V19_FAR                                                                                 \
-    "L%=_far:\n\t"                                                                                   \
-    "s_and_b32 %[s1], %[c], -4\n\t"                                                                 \
-    "v_add_u32_e32 %[t1], %[s1], %[lane4]\n\t"                                                      \
-    "global_load_dword %[t3], %[t1], %[srcb]\n\t"                                                   \
-    "s_mov_b32 %[s1], 0x10203\n\t"                                                                  \
-    "s_waitcnt vmcnt(0)\n\t"                                                                        \
-    "v_perm_b32 %[t3], %[t3], %[t3], %[s1]\n\t" /* big-endian, as the ring registers */             \
-    "s_branch L%=_farret\n"
-#else
-#define K1R_V19_TARGET "x3"
-#define K1R_V19_FAR
-#endif
-// SNAPPY_K1R64_CAND (A/B, 1 GiB of 64 KiB text blocks, outputs identical,
-// profiles/r05b_ab_*, r05c_ab_*): 0 = the two tests as shifts and compares of
-// the segment index (18.70 ms); 1 = the residency test as one compare of the
-// candidate against the lowest resident position (seghi carries (seg_hi - 128)
-// * 256) and the segment's register by one s_bfe (18.08-18.16 ms, kept);
-// 2 = no tests (measurement only, wrong output: 17.55 ms, the most the tests
-// can cost); 3 = as 1 with the wrap pair 127 / 0 read branch-free (a
-// scalar-mask select of v2; 18.19-18.23 ms, random 1 % faster)
-#ifndef SNAPPY_K1R64_CAND
-#define SNAPPY_K1R64_CAND 1
-#endif
-#if SNAPPY_K1R64_CAND == 0
-#define K1R_CAND64                                                                                  \
-    "s_lshr_b32 %[s0], %[c], 8\n\t"                                                                \
-    "s_add_u32 %[s1], %[s0], 128\n\t"                                                              \
-    "s_cmp_lt_u32 %[s1], %[seghi]\n\t"                                                             \
-    "s_cbranch_scc1 L%=_x3\n\t"                                                                    \
-    "s_and_b32 %[s0], %[s0], 127\n\t"                                                              \
-    "s_cmp_eq_u32 %[s0], 127\n\t"                                                                  \
-    "s_cbranch_scc1 L%=_x3\n\t"
-#define K1R_SEGHI64(seg_hi) "s"(seg_hi)
-#elif SNAPPY_K1R64_CAND == 1
+// K1r64: residency as one compare of c against the first resident position
+// (seghi = (seg_hi - 128) * 256; r05b_ab_k4_k1r64_cand_text64k.log: 18.70 ->
+// 18.08 ms per GiB), the segment's register by one s_bfe
 #define K1R_CAND64                                                                                  \
     "s_cmp_lt_u32 %[c], %[seghi]\n\t"                                                              \
-    "s_cbranch_scc1 L%=_" K1R_V19_TARGET "\n\t"                                                     \
+    "s_cbranch_scc1 L%=_far\n\t"                                                                   \
     "s_bfe_u32 %[s0], %[c], 0x70008\n\t"                                                           \
     "s_cmp_eq_u32 %[s0], 127\n\t"                                                                  \
     "s_cbranch_scc1 L%=_x3\n\t"
 #define K1R_SEGHI64(seg_hi) "s"(((seg_hi) - kRegs) << 8)
-#elif SNAPPY_K1R64_CAND == 3
-// the residency test as in 1; the wrap pair 127 / 0 without a branch: the
-// second register of the pair is ring register 0 (v2) when the first is 127
-// (the indexed pair read v130 there), selected by a scalar mask
-#define K1R_CAND64                                                                                  \
-    "s_cmp_lt_u32 %[c], %[seghi]\n\t"                                                              \
-    "s_cbranch_scc1 L%=_x3\n\t"                                                                    \
-    "s_bfe_u32 %[s0], %[c], 0x70008\n\t"                                                           \
-    "s_cmp_eq_u32 %[s0], 127\n\t"                                                                  \
-    "s_cselect_b64 %[wm], -1, 0\n\t"
-#define K1R_WRAP64 "v_cndmask_b32_e64 %[t4], %[t4], v2, %[wm]\n\t"
-#define K1R_SEGHI64(seg_hi) "s"(((seg_hi) - kRegs) << 8)
-#else
-#define K1R_CAND64 "s_bfe_u32 %[s0], %[c], 0x70008\n\t"
-#define K1R_SEGHI64(seg_hi) "i"(0)
-#endif
-#ifndef K1R_WRAP64
-#define K1R_WRAP64 ""
-#endif
-// SNAPPY_K1R_ASM_V2 (A/B): the hit path with fewer scalar instructions on the
-// round's dependency chain: the hit branch on the SCC of the s_and that makes
-// the hit mask; the candidate used unmasked (it is < 65,536: a u16 table entry
-// or a position) and the gather addresses without clearing their low bits
-// (ds_bpermute reads addr[7:2], and adding 4 x lane never carries out of bits
-// 0-1); the first differing dword found by one s_ff1 of vcc_lo (> 15 or -1 =
-// 64 equal bytes); the next lane0 as f + length; one signed compare against
-// lim0 = min(62 - RMIN, L - 16 - q0) for "continue", the exit decided after it
-#ifndef SNAPPY_K1R_ASM_V2
-#define SNAPPY_K1R_ASM_V2 1
-#endif
-// SNAPPY_K1R_ASM_V3 (with V2): the prefix length with fewer VALU before its
-// v_readlane: (clz(xor) | 32 x lane) read back, divided by 8 in SALU (lanes
-// with equal dwords are never read, so no `| 1` guard on the clz)
-#ifndef SNAPPY_K1R_ASM_V3
-#define SNAPPY_K1R_ASM_V3 1
-#endif
-// SNAPPY_K1R_ASM_V4: the hit mask in SALU from two lane masks -- the table
-// lanes' tag hits (one SDWA compare to an SGPR pair) and pdz, the lanes whose
-// in-window predecessor's tag matches (per window) -- instead of a VALU select
-// of the two tag differences and a compare
-#ifndef SNAPPY_K1R_ASM_V4
-#define SNAPPY_K1R_ASM_V4 0
-#endif
-#define K1R_HIT_V16                                                                                 \
-    "v_cndmask_b32_sdwa %[t1], %[pdc], %[ent], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "             \
-    "src0_sel:DWORD src1_sel:WORD_0\n\t" /* the candidate of every lane */                          \
-    "v_cndmask_b32_e32 %[t0], %[pdnz], %[entt], vcc\n\t" /* and its tag */                          \
-    "v_cmp_eq_u32_sdwa %[hm], %[t0], %[word] src0_sel:DWORD src1_sel:WORD_1\n\t"
-
-#if SNAPPY_K1R_ASM_V4
-#define K1R_V4_HIT                                                                                  \
-    "v_cmp_eq_u32_sdwa %[hm], %[entt], %[word] src0_sel:DWORD src1_sel:WORD_1\n\t"                   \
-    "v_cndmask_b32_sdwa %[t1], %[pdc], %[ent], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "             \
-    "src0_sel:DWORD src1_sel:WORD_0\n\t" /* the candidate of every lane */                          \
-    "s_andn2_b64 %[wm], %[pdz], vcc\n\t"                                                            \
-    "s_and_b64 %[hm], %[hm], vcc\n\t"                                                               \
-    "s_or_b64 %[hm], %[hm], %[wm]\n\t"
-#else
-#define K1R_V4_HIT                                                                                  \
+#define K1R_HIT_TAGDIFF                                                                             \
     "v_xor_b32_sdwa %[t0], %[entt], %[word] dst_sel:DWORD dst_unused:UNUSED_PAD "                    \
     "src0_sel:DWORD src1_sel:WORD_1\n\t"                                                            \
     "v_cndmask_b32_sdwa %[t1], %[pdc], %[ent], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "             \
     "src0_sel:DWORD src1_sel:WORD_0\n\t" /* the candidate of every lane */                          \
     "v_cndmask_b32_sdwa %[t0], %[pdnz], %[t0], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "             \
-    "src0_sel:DWORD src1_sel:" K1R_V6_T0SEL "\n\t"                                                   \
+    "src0_sel:DWORD src1_sel:WORD_0\n\t"                                                            \
     "v_cmp_eq_u32_e64 %[hm], 0, %[t0]\n\t"
-#endif
-// SNAPPY_K1R_ASM_V5 (with V2/V3): three scalar instructions fewer per hit round:
-// the candidate pair's lane select by a VALU compare into vcc (free between the
-// round's two uses of it) instead of a 64-bit shifted mask; lo0 = lane0 - (lane0
-// < f) by s_subb on the compare's SCC; dkn not cleared after the drain (the hit
-// round sets it to 1 before the loop goes on; the C++ finish of codes 4 and 5
-// sets it itself)
-#ifndef SNAPPY_K1R_ASM_V5
-#define SNAPPY_K1R_ASM_V5 1
-#endif
-#if SNAPPY_K1R_ASM_V5
-#define K1R_V5_ROT "v_cmp_le_u32_e32 vcc, %[s1], %[lane]\n\t" /* lanes >= l0 take register R */
-#define K1R_V5_SEL "v_cndmask_b32_e32 %[t3], %[t4], %[t3], vcc\n\t"
-#define K1R_V5_LO0                                                                                  \
-    "s_cmp_lt_u32 %[lane0], %[f]\n\t"                                                               \
-    "s_subb_u32 %[s0], %[lane0], 0\n\t" /* lo0 */
-#else
-#define K1R_V5_ROT "s_lshl_b64 %[hm], -1, %[s1]\n\t" /* lanes >= l0 take register R */
-#define K1R_V5_SEL "v_cndmask_b32_e64 %[t3], %[t4], %[t3], %[hm]\n\t"
-#define K1R_V5_LO0                                                                                  \
-    "s_mov_b32 %[dkn], 0\n\t"                                                                       \
-    "s_add_i32 %[s0], %[lane0], -1\n\t"                                                             \
-    "s_cmp_lt_u32 %[lane0], %[f]\n\t"                                                               \
-    "s_cselect_b32 %[s0], %[s0], %[lane0]\n\t" /* lo0 */
-#endif
-// SNAPPY_K1R_ASM_V6 (with V2/V3/V5): five more scalar instructions off the hit
-// round: the window mask folded into the per-window lane data (a lane past the
-// window gets bit 24 of its insert word -- its tag compare then differs in bit
-// 8 -- and a non-zero pdnz), so only the miss path still ands it into `valid`;
-// the dwords at pf gathered from (pf - 1) / 4 and funnelled by v_alignbit with
-// the scalar shift -8 pf (bits 4:0 = 32 - 8 (pf % 4), and 0 takes the next
-// dword: the one at pf when pf % 4 == 0), one s_mul instead of an and, a
-// multiply and an add for a perm selector; the clamp of the match length to
-// the block end only on the exit path (the continue test lane0 <= lim0 already
-// implies pf + len <= L - 16)
-#ifndef SNAPPY_K1R_ASM_V6
-#define SNAPPY_K1R_ASM_V6 1
-#endif
-#if SNAPPY_K1R_ASM_V6
-#define K1R_V6_MWIN_HIT ""
-#define K1R_V6_MWIN_NOHIT "s_and_b64 %[valid], %[valid], %[mwin]\n\t"
-#define K1R_V6_T0SEL "WORD_0"
-#define K1R_V6_SEL2A "s_mul_i32 %[s2], %[pf], -8\n\t"
-#define K1R_V6_SEL2B ""
-#define K1R_V6_FUNNEL_PA "v_alignbit_b32 %[t2], %[t2], %[t1], %[s2]\n\t"
-#define K1R_V6_DRAIN                                                                                \
-    "s_mov_b32 m0, %[pend]\n\t" /* (gfx950 refuses two SGPRs in a v_writelane: m0 stays) */          \
-    "v_writelane_b32 %[tka], %[dka], m0\n\t"                                                        \
-    "v_writelane_b32 %[tkb], %[dkb], m0\n\t"
-#else
-#define K1R_V6_MWIN_HIT "s_and_b64 %[valid], %[valid], %[mwin]\n\t"
-#define K1R_V6_MWIN_NOHIT ""
-#define K1R_V6_T0SEL "BYTE_0"
-#define K1R_V6_SEL2A "s_and_b32 %[s2], %[pf], 3\n\ts_mul_i32 %[s2], %[s2], 0xfefefeff\n\t"
-#define K1R_V6_SEL2B "s_add_i32 %[s2], %[s2], 0x7060504\n\t"
-#define K1R_V6_FUNNEL_PA "v_perm_b32 %[t2], %[t2], %[t1], %[s2]\n\t"
-#define K1R_V6_DRAIN                                                                                \
-    "s_mov_b32 m0, %[pend]\n\t"                                                                     \
-    "v_writelane_b32 %[tka], %[dka], m0\n\t"                                                        \
-    "v_writelane_b32 %[tkb], %[dkb], m0\n\t"
-#endif
-#if SNAPPY_K1R_ASM_V2 && SNAPPY_K1R_ASM_V3
-#define K1R_V3_LEN                                                                                  \
-    "v_xor_b32_e32 %[t2], %[t2], %[t3]\n\t"                                                         \
-    "v_ffbh_u32_e32 %[t2], %[t2]\n\t"                                                               \
-    "v_lshl_or_b32 %[t2], %[lane4], 3, %[t2]\n\t" /* 8 x the prefix length if this dword differs */
-#define K1R_V3_DIV "s_lshr_b32 %[s0], %[s0], 3\n\t"
-#else
-#define K1R_V3_LEN                                                                                  \
-    "v_xor_b32_e32 %[t2], %[t2], %[t3]\n\t"                                                         \
-    "v_or_b32_e32 %[t2], 1, %[t2]\n\t"                                                              \
-    "v_ffbh_u32_e32 %[t2], %[t2]\n\t"                                                               \
-    "v_lshrrev_b32_e32 %[t2], 3, %[t2]\n\t"                                                         \
-    "v_or_b32_e32 %[t2], %[t2], %[lane4]\n\t" /* the prefix length if this dword differs */
-#define K1R_V3_DIV ""
-#endif
-// SNAPPY_K1R_ASM_V7 (with V6): p (read only after the loop) is set on the exit
-// path alone, and the prefix length comes back from v_readlane finished
-// ((clz >> 3) | 4 x lane by v_bfe + v_lshl_or) instead of a scalar division
-#ifndef SNAPPY_K1R_ASM_V7
-#define SNAPPY_K1R_ASM_V7 1
-#endif
-// SNAPPY_K1R_ASM_V8 (with V6): skip is not reset by a hit round.  Everywhere,
-// dkn == 1 (a match's token pending) comes with skip == 32 (the C++ code sets
-// both together), so the loop keeps skip stale after a hit and the miss path
-// and the loop's exit take 32 whenever dkn is 1
-#ifndef SNAPPY_K1R_ASM_V8
-#define SNAPPY_K1R_ASM_V8 1
-#endif
-#if SNAPPY_K1R_ASM_V8
-#define K1R_V8_SKIP ""
-#define K1R_V8_SKIPFIX "s_cmp_eq_u32 %[dkn], 0\n\ts_cselect_b32 %[skip], %[skip], 32\n\t"
-#else
-#define K1R_V8_SKIP "s_mov_b32 %[skip], 32\n\t"
-#define K1R_V8_SKIPFIX ""
-#endif
-// SNAPPY_K1R_ASM_V9 (with V8): the deferred token's first word by one
-// s_pack_ll_b32_b16 (pf and the length are < 2^16); the miss path does not
-// clear dka / dkb (with dkn = 0 the next drain writes lane pend, which the
-// next token overwrites) and steps lane0 first, p = q0 + lane0 from it
-#ifndef SNAPPY_K1R_ASM_V9
-#define SNAPPY_K1R_ASM_V9 1
-#endif
-#if SNAPPY_K1R_ASM_V9
-#define K1R_V9_DKA "s_pack_ll_b32_b16 %[dka], %[pf], %[s0]\n\t"
-#define K1R_V9_DKZERO ""
-#define K1R_V9_NOHIT_P                                                                              \
-    "s_add_u32 %[lane0], %[s1], %[s0]\n\t" /* lane0 - 1 + nk + the step-2 probe */                 \
-    "s_add_u32 %[lane0], %[lane0], %[s3]\n\t"                                                       \
-    "s_add_u32 %[p], %[q0], %[lane0]\n\t"
-#define K1R_V9_NOHIT_L0 ""
-#else
-#define K1R_V9_DKA "s_lshl_b32 %[s1], %[s0], 16\n\ts_or_b32 %[dka], %[s1], %[pf]\n\t"
-#define K1R_V9_DKZERO "s_mov_b32 %[dka], 0\n\ts_mov_b32 %[dkb], 0\n\t"
-#define K1R_V9_NOHIT_P                                                                              \
-    "s_add_u32 %[p], %[q0], %[lane0]\n\t"                                                           \
-    "s_add_u32 %[p], %[p], %[s0]\n\t"                                                               \
-    "s_add_u32 %[p], %[p], %[s3]\n\t"                                                               \
-    "s_add_i32 %[p], %[p], -1\n\t"
-#define K1R_V9_NOHIT_L0 "s_sub_u32 %[lane0], %[p], %[q0]\n\t"
-#endif
-// SNAPPY_K1R_ASM_V10 (with V6): the dwords-at-pf funnel shift -8 pf by
-// v_mul_i32_i24 into a free VGPR instead of s_mul (bits 4:0 are all v_alignbit
-// reads).  (v_movrels_b32 for the candidate's register pair, which would save
-// the s_set_gpr_idx pair, does not exist on gfx950.)
-#ifndef SNAPPY_K1R_ASM_V10
-#define SNAPPY_K1R_ASM_V10 1
-#endif
-#define K1R_V10_PAIR                                                                                \
-    "s_set_gpr_idx_on %[s0], gpr_idx(SRC0)\n\t"                                                     \
-    "v_mov_b32_e32 %[t3], v2\n\t"                                                                   \
-    "v_mov_b32_e32 %[t4], v3\n\t"                                                                   \
-    "s_set_gpr_idx_off\n\t"                                                                         \
-    "s_bfe_u32 %[s1], %[c], 0x60002\n\t"
-// SNAPPY_K1R_ASM_V15: the candidate's register pair selected by one indexed
-// v_cndmask (s_set_gpr_idx with SRC0 and SRC1: lanes >= l0 take register R,
-// the others R + 1) instead of two indexed moves and a select (65,536-byte
-// blocks leave the loop at the wrap pair 127 / 0, SNAPPY_K1R64_CAND 1)
-#ifndef SNAPPY_K1R_ASM_V15
-#define SNAPPY_K1R_ASM_V15 1
-#endif
-#if SNAPPY_K1R_ASM_V15 && SNAPPY_K1R64_CAND != 3
-#undef K1R_V10_PAIR
-#define K1R_V10_PAIR                                                                                \
-    "s_bfe_u32 %[s1], %[c], 0x60002\n\t"                                                            \
-    "v_cmp_le_u32_e32 vcc, %[s1], %[lane]\n\t" /* lanes >= l0 take register R */                   \
-    "v_add_u32_e32 %[t1], %[c], %[lane4]\n\t"                                                      \
-    "s_set_gpr_idx_on %[s0], gpr_idx(SRC0,SRC1)\n\t"                                               \
-    "v_cndmask_b32_e32 %[t3], v3, v2, vcc\n\t"                                                     \
-    "s_set_gpr_idx_off\n\t"
-#undef K1R_V5_ROT
-#define K1R_V5_ROT ""
-#undef K1R_V5_SEL
-#define K1R_V5_SEL ""
-#define K1R_V15_CA ""
-#else
-#define K1R_V15_CA K1R_V2_CA
-#endif
-#if SNAPPY_K1R_ASM_V10
-#define K1R_V10_SEL2A "v_mul_i32_i24_e64 %[t0], %[pf], -8\n\t"
-#define K1R_V10_FUNNEL_PA "v_alignbit_b32 %[t2], %[t2], %[t1], %[t0]\n\t"
-#else
-#define K1R_V10_SEL2A K1R_V6_SEL2A
-#define K1R_V10_FUNNEL_PA K1R_V6_FUNNEL_PA
-#endif
-// SNAPPY_K1R_ASM_V11: the candidate funnel's perm selector 0x07060504 - (c % 4)
-// x 0x01010101 in VALU (and, u24 multiply, lshl_or, sub: two more VGPRs)
-// instead of s_and / s_mul / s_add
-#ifndef SNAPPY_K1R_ASM_V11
-#define SNAPPY_K1R_ASM_V11 0
-#endif
-#if SNAPPY_K1R_ASM_V11
-#define K1R_V11_SEL3                                                                                \
-    "v_and_b32_e64 %[t5], %[c], 3\n\t"                                                              \
-    "v_mul_u32_u24_e32 %[t6], 0x10101, %[t5]\n\t"                                                   \
-    "v_lshl_or_b32 %[t5], %[t6], 8, %[t5]\n\t" /* (c % 4) x 0x01010101 */                         \
-    "v_sub_u32_e32 %[t5], 0x7060504, %[t5]\n\t"
-#define K1R_V11_PERM3 "v_perm_b32 %[t3], %[t3], %[t4], %[t5]\n\t"
-#define K1R_V11_OUTS , [t5] "=&v"(_t5), [t6] "=&v"(_t6)
-#else
-#define K1R_V11_SEL3                                                                                \
-    "s_and_b32 %[s3], %[c], 3\n\t"                                                                  \
-    "s_mul_i32 %[s3], %[s3], 0xfefefeff\n\t"                                                        \
-    "s_add_i32 %[s3], %[s3], 0x7060504\n\t"
-#define K1R_V11_PERM3 "v_perm_b32 %[t3], %[t3], %[t4], %[s3]\n\t"
-#define K1R_V11_OUTS
-#endif
-// SNAPPY_K1R_ASM_V13: the inserts under an exec mask made by one s_bfm_b64
-// (the round loop runs in uniform control flow with all 64 lanes of the wave
-// live, so it restores exec to all ones; exec cannot be declared clobbered)
-// (lanes lo0 .. f; a missing round's lane0 - 1 .. lane0 - 1 + nk: at most DMAX +
-// 1 lanes, so the 6-bit size never wraps) instead of every lane writing its
-// record or the shared dummy: four VALU (range compare, address select, tag
-// address) for three SALU, and no same-address writes
-// SNAPPY_K1R_ASM_V20 (32 KiB units): the pa gather address as f + lq, lq = q0 -
-// 1 + 4 lane per asm entry, so the scalar pf = q0 + f leaves the gather's chain
-#ifndef SNAPPY_K1R_ASM_V20
-#define SNAPPY_K1R_ASM_V20 0
-#endif
-#define K1R_PA64                                                                                    \
-    "v_readlane_b32 %[c], %[t1], %[f]\n\t"                                                          \
-    "s_add_u32 %[pf], %[q0], %[f]\n\t" K1R_V2_PA                                                    \
-    "ds_bpermute_b32 %[t2], %[t2], %[dv]\n\t" /* pa: dwords at pf */
-#if SNAPPY_K1R_ASM_V20 && SNAPPY_K1R_ASM_V6
-// (and the pa gather issued before the candidate's read-back)
-#define K1R_PA32                                                                                    \
-    "v_add_u32_e32 %[t2], %[f], %[lq]\n\t" /* dwords from (pf - 1) / 4: see V6 */                  \
-    "ds_bpermute_b32 %[t2], %[t2], %[dv]\n\t" /* pa: dwords at pf */                                \
-    "v_readlane_b32 %[c], %[t1], %[f]\n\t"                                                          \
-    "s_add_u32 %[pf], %[q0], %[f]\n\t"
-#define K1R_LQ32 (lane << 2) + q0 - 1
-#else
-#define K1R_PA32 K1R_PA64
-#define K1R_LQ32 lane << 2
-#endif
+#define K1R_HIT_PREDTAG                                                                             \
+    "v_cndmask_b32_sdwa %[t1], %[pdc], %[ent], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "             \
+    "src0_sel:DWORD src1_sel:WORD_0\n\t" /* the candidate of every lane */                          \
+    "v_cndmask_b32_e32 %[t0], %[pdnz], %[entt], vcc\n\t" /* and its tag */                          \
+    "v_cmp_eq_u32_sdwa %[hm], %[t0], %[word] src0_sel:DWORD src1_sel:WORD_1\n\t"
 #if SNAPPY_K1R_ASM_V16 == 1
-#define K1R_HIT32 K1R_HIT_V16
+#define K1R_HIT32 K1R_HIT_PREDTAG
 #else
-#define K1R_HIT32 K1R_V4_HIT
+#define K1R_HIT32 K1R_HIT_TAGDIFF
 #endif
 #if SNAPPY_K1R_ASM_V16 >= 1
-#define K1R_HIT64 K1R_HIT_V16
+#define K1R_HIT64 K1R_HIT_PREDTAG
 #else
-#define K1R_HIT64 K1R_V4_HIT
+#define K1R_HIT64 K1R_HIT_TAGDIFF
 #endif
-#ifndef SNAPPY_K1R_ASM_V13
-#define SNAPPY_K1R_ASM_V13 1
-#endif
-// SNAPPY_K1R_ASM_V14 (with V13): a hit round reads the next round's entries
-// only in lanes > f (exec), inside the inserts' exec window
-#ifndef SNAPPY_K1R_ASM_V14
-#define SNAPPY_K1R_ASM_V14 0
-#endif
-#if SNAPPY_K1R_ASM_V13 && SNAPPY_K1R_ASM_V14
-#define K1R_V14_READ_MASK                                                                           \
-    "s_add_u32 %[s2], %[f], 1\n\t"                                                                  \
-    "s_lshl_b64 exec, -1, %[s2]\n\t" /* lanes > f (f <= 62) */                                     \
-    "ds_read_u16 %[ent], %[adr]\n\t"                                                                \
-    "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"
-#define K1R_V14_SKIP_READS 1
-#else
-#define K1R_V14_READ_MASK
-#define K1R_V14_SKIP_READS 0
-#endif
-#if SNAPPY_K1R_ASM_V13
-#define K1R_V13_DUMMY_IN
-#define K1R_V13_HIT_INSERT                                                                          \
-    K1R_V10_SEL2A /* (a VALU result every lane needs: before the exec change) */                   \
-    "s_sub_u32 %[s2], %[f], %[s0]\n\t"                                                              \
-    "s_add_u32 %[s2], %[s2], 1\n\t"                                                                 \
-    "s_bfm_b64 exec, %[s2], %[s0]\n\t" /* lanes lo0 .. f */                                         \
-    "ds_write_b16 %[adr], %[word]\n\t"                                                              \
-    "ds_write_b8_d16_hi %[adrt], %[word] offset:%[tagb]\n\t"                                        \
-    K1R_V14_READ_MASK                                                                               \
-    "s_mov_b64 exec, -1\n\t"
-#define K1R_V13_NOHIT_INSERT                                                                        \
-    "s_add_u32 %[s2], %[skip], %[s0]\n\t"                                                           \
-    "s_add_i32 %[s3], %[s2], -1\n\t"                                                                \
-    "s_add_u32 %[c], %[s0], 1\n\t" /* (c is free on this path) */                                  \
-    "s_bfm_b64 exec, %[c], %[s1]\n\t" /* lanes lane0 - 1 .. lane0 - 1 + nk */                      \
-    "ds_write_b16 %[adr], %[word]\n\t"                                                              \
-    "ds_write_b8_d16_hi %[adrt], %[word] offset:%[tagb]\n\t"                                        \
-    "s_mov_b64 exec, -1\n\t"
-#else
-#define K1R_V13_DUMMY_IN , [dummy] "v"(kDummy)
-#define K1R_V13_HIT_INSERT                                                                          \
-    "v_subrev_u32_e32 %[t4], %[s0], %[lane]\n\t"                                                    \
-    "s_sub_u32 %[s0], %[f], %[s0]\n\t"                                                              \
-    "v_cmp_ge_u32_e32 vcc, %[s0], %[t4]\n\t" /* lanes lo0 .. f insert */                            \
-    K1R_V10_SEL2A                                                                                   \
-    "v_cndmask_b32_e32 %[t4], %[dummy], %[adr], vcc\n\t"                                            \
-    "ds_write_b16 %[t4], %[word]\n\t"                                                               \
-    "v_lshrrev_b32_e32 %[t4], 1, %[t4]\n\t"                                                         \
-    "ds_write_b8_d16_hi %[t4], %[word] offset:%[tagb]\n\t"
-#define K1R_V13_NOHIT_INSERT                                                                        \
-    "v_subrev_u32_e32 %[t4], %[s1], %[lane]\n\t"                                                    \
-    "v_cmp_ge_u32_e32 vcc, %[s0], %[t4]\n\t"                                                        \
-    "s_add_u32 %[s2], %[skip], %[s0]\n\t"                                                           \
-    "s_add_i32 %[s3], %[s2], -1\n\t"                                                                \
-    "v_cndmask_b32_e32 %[t4], %[dummy], %[adr], vcc\n\t"                                            \
-    "ds_write_b16 %[t4], %[word]\n\t"                                                               \
-    "v_lshrrev_b32_e32 %[t4], 1, %[t4]\n\t"                                                         \
-    "ds_write_b8_d16_hi %[t4], %[word] offset:%[tagb]\n\t"
-#endif
-// SNAPPY_K1R_ASM_V18 (with V13): a hit round's inserts and entry reads issued
-// after the wait for the two gathers (and behind the funnels), so that wait no
-// longer covers the insert writes; they complete during the verification (A/B,
-// outputs identical, profiles/r05zf_*: 32 KiB streams 12.89 -> 12.69 ms per GiB,
-// 64 KiB blocks 14.50 -> 14.23-14.28)
-#ifndef SNAPPY_K1R_ASM_V18
-#define SNAPPY_K1R_ASM_V18 1
-#endif
-#if SNAPPY_K1R_ASM_V18 && SNAPPY_K1R_ASM_V13 && !SNAPPY_K1R_ASM_V14 && !SNAPPY_K1R_ASM_V12
-#define K1R_V18_PRE                                                                                 \
-    K1R_V10_SEL2A                                                                                   \
-    "s_sub_u32 %[s2], %[f], %[s0]\n\t"                                                              \
-    "s_add_u32 %[s2], %[s2], 1\n\t"                                                                 \
-    K1R_V11_SEL3
-#define K1R_V18_WAIT "s_waitcnt lgkmcnt(0)\n\t" /* pa and ca */
-#define K1R_V18_POST                                                                                \
-    "s_bfm_b64 exec, %[s2], %[s0]\n\t" /* lanes lo0 .. f insert */                                  \
-    "ds_write_b16 %[adr], %[word]\n\t"                                                              \
-    "ds_write_b8_d16_hi %[adrt], %[word] offset:%[tagb]\n\t"                                        \
-    "s_mov_b64 exec, -1\n\t"                                                                        \
-    "ds_read_u16 %[ent], %[adr]\n\t"                                                                \
-    "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"
-// (placing them after the match length's read-back instead, with lo0 kept in
-// s3: 32 KiB streams -1.3 %, 64 KiB blocks +1.8 % against this placement;
-// its s3 copy alone cost 0.6 %: profiles/r05zg_*)
-#define K1R_V18_MID
-#define K1R_V18_X4
-#else
-#define K1R_V18_PRE K1R_V13_HIT_INSERT K1R_V12_READS
-#define K1R_V18_WAIT "s_waitcnt lgkmcnt(2)\n\t" /* pa, ca and the inserts; the entry reads stay in flight */
-#define K1R_V18_POST
-#define K1R_V18_MID
-#define K1R_V18_X4
-#endif
-// SNAPPY_K1R_ASM_V12: a hit round's entry reads only for lanes > f (the next
-// round starts at f + len >= f + 4); lanes <= f read the dummy record (one
-// address: a broadcast, no bank conflicts -- K1r's LDS spent 38 % of its active
-// cycles in bank conflicts, profiles/r05v_*).  The SEL3 scalar instructions fill
-// the compare's two wait states before the select reads vcc
-#ifndef SNAPPY_K1R_ASM_V12
-#define SNAPPY_K1R_ASM_V12 0
-#endif
-#if SNAPPY_K1R_ASM_V12
-#define K1R_V12_READS                                                                               \
-    "v_cmp_lt_u32_e32 vcc, %[f], %[lane]\n\t"                                                      \
-    K1R_V11_SEL3                                                                                    \
-    "v_cndmask_b32_e32 %[t4], %[dummy], %[adr], vcc\n\t"                                            \
-    "ds_read_u16 %[ent], %[t4]\n\t"                                                                \
-    "v_lshrrev_b32_e32 %[t4], 1, %[t4]\n\t"                                                        \
-    "ds_read_u8 %[entt], %[t4] offset:%[tagb]\n\t"
-#elif K1R_V14_SKIP_READS
-#define K1R_V12_READS K1R_V11_SEL3
-#else
-#define K1R_V12_READS                                                                               \
-    "ds_read_u16 %[ent], %[adr]\n\t"                                                               \
-    "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"                                               \
-    K1R_V11_SEL3
-#endif
-#if SNAPPY_K1R_ASM_V7
-#define K1R_V7_P ""
-#undef K1R_V3_LEN
-#undef K1R_V3_DIV
-#define K1R_V3_LEN                                                                                  \
-    "v_xor_b32_e32 %[t2], %[t2], %[t3]\n\t"                                                         \
-    "v_ffbh_u32_e32 %[t2], %[t2]\n\t"                                                               \
-    "v_bfe_u32 %[t2], %[t2], 3, 2\n\t"                                                              \
-    "v_lshl_or_b32 %[t2], %[lane], 2, %[t2]\n\t" /* the prefix length if this dword differs */
-#define K1R_V3_DIV ""
-#else
-#define K1R_V7_P "s_add_u32 %[p], %[pf], %[s0]\n\t"
-#endif
-// SNAPPY_K1R_ASM_V17 (with V7): the prefix length from the first differing
-// dword's xor read back and finished in SALU (s_flbit, s_lshr, s_lshl2_add)
-// instead of ffbh / bfe / lshl_or on every lane
-#ifndef SNAPPY_K1R_ASM_V17
-#define SNAPPY_K1R_ASM_V17 0
-#endif
-#if SNAPPY_K1R_ASM_V7 && SNAPPY_K1R_ASM_V17
-#undef K1R_V3_LEN
-#undef K1R_V3_DIV
-#define K1R_V3_LEN "v_xor_b32_e32 %[t2], %[t2], %[t3]\n\t"
-#define K1R_V3_DIV                                                                                  \
-    "s_flbit_i32_b32 %[s0], %[s0]\n\t"                                                              \
-    "s_lshr_b32 %[s0], %[s0], 3\n\t"                                                                \
-    "s_lshl2_add_u32 %[s0], %[s1], %[s0]\n\t" /* 4 k + the equal bytes of dword k */
-#endif
-#if SNAPPY_K1R_ASM_V2 && SNAPPY_K1R_ASM_V6
-#define K1R_V2_TAIL                                                                                 \
-    "s_ff1_i32_b32 %[s1], vcc_lo\n\t"                                                               \
-    "s_cmp_gt_u32 %[s1], 15\n\t"                                                                    \
-    "s_cbranch_scc1 L%=_x4\n\t"                                                                     \
-    "v_readlane_b32 %[s0], %[t2], %[s1]\n\t"                                                        \
-    K1R_V3_DIV                                                                                      \
-    K1R_V18_MID                                                                                     \
-    "s_cmp_lt_u32 %[s0], 4\n\t" /* (pf <= L - 16: the clamp below never makes it < 4) */            \
-    "s_cbranch_scc1 L%=_x5\n\t"                                                                     \
-    "s_add_u32 %[lane0], %[f], %[s0]\n\t"                                                           \
-    K1R_V7_P                                                                                        \
-    K1R_V9_DKA                                                                                      \
-    "s_sub_u32 %[dkb], %[pf], %[c]\n\t"                                                             \
-    "s_mov_b32 %[dkn], 1\n\t"                                                                       \
-    K1R_V8_SKIP                                                                                     \
-    "s_cmp_le_i32 %[lane0], %[lim0]\n\t" /* implies pf + len <= L - 16: no clamp */                 \
-    "s_cbranch_scc1 L%=_top\n\t"                                                                    \
-    "s_sub_u32 %[s2], %[L], %[pf]\n\t" /* leaving: the length clamped to the block end */         \
-    "s_min_u32 %[s0], %[s0], %[s2]\n\t"                                                             \
-    "s_add_u32 %[p], %[pf], %[s0]\n\t"                                                              \
-    "s_sub_u32 %[lane0], %[p], %[q0]\n\t"                                                           \
-    "s_lshl_b32 %[s1], %[s0], 16\n\t"                                                               \
-    "s_or_b32 %[dka], %[s1], %[pf]\n\t"                                                             \
-    "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                                \
-    "s_cbranch_scc1 L%=_x1\n\t"                                                                     \
-    "s_branch L%=_x2\n"
-#endif
-#if SNAPPY_K1R_ASM_V2
-#define K1R_V2_HITBR "s_cbranch_scc0 L%=_nohit\n\t" /* SCC = (hm != 0) */
-#if SNAPPY_K1R_ASM_V6
-#define K1R_V2_PA "v_add3_u32 %[t2], %[pf], -1, %[lane4]\n\t" /* dwords from (pf - 1) / 4: see V6 */
-#else
-#define K1R_V2_PA "v_add_u32_e32 %[t2], %[pf], %[lane4]\n\t"
-#endif
-#define K1R_V2_CMASK ""
-#define K1R_V2_CA "v_add_u32_e32 %[t1], %[c], %[lane4]\n\t"
-#ifndef K1R_V2_TAIL
-#define K1R_V2_TAIL                                                                                 \
-    "s_sub_u32 %[s2], %[L], %[pf]\n\t"                                                              \
-    "s_ff1_i32_b32 %[s1], vcc_lo\n\t"                                                               \
-    "s_cmp_gt_u32 %[s1], 15\n\t"                                                                    \
-    "s_cbranch_scc1 L%=_x4\n\t"                                                                     \
-    "v_readlane_b32 %[s0], %[t2], %[s1]\n\t"                                                        \
-    K1R_V3_DIV                                                                                      \
-    "s_min_u32 %[s0], %[s0], %[s2]\n\t"                                                             \
-    "s_cmp_lt_u32 %[s0], 4\n\t"                                                                     \
-    "s_cbranch_scc1 L%=_x5\n\t"                                                                     \
-    "s_add_u32 %[lane0], %[f], %[s0]\n\t"                                                           \
-    "s_add_u32 %[p], %[pf], %[s0]\n\t"                                                              \
-    "s_lshl_b32 %[s1], %[s0], 16\n\t"                                                               \
-    "s_or_b32 %[dka], %[s1], %[pf]\n\t"                                                             \
-    "s_sub_u32 %[dkb], %[pf], %[c]\n\t"                                                             \
-    "s_mov_b32 %[dkn], 1\n\t"                                                                       \
-    "s_mov_b32 %[skip], 32\n\t"                                                                     \
-    "s_cmp_le_i32 %[lane0], %[lim0]\n\t"                                                            \
-    "s_cbranch_scc1 L%=_top\n\t"                                                                    \
-    "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                                \
-    "s_cbranch_scc1 L%=_x1\n\t"                                                                     \
-    "s_branch L%=_x2\n"
-#endif
-#else
-#define K1R_V2_HITBR "s_cmp_eq_u64 %[hm], 0\n\ts_cbranch_scc1 L%=_nohit\n\t"
-#define K1R_V2_PA "s_and_b32 %[s0], %[pf], -4\n\tv_add_u32_e32 %[t2], %[s0], %[lane4]\n\t"
-#define K1R_V2_CMASK "s_and_b32 %[c], %[c], 0xffff\n\t"
-#define K1R_V2_CA "s_and_b32 %[s0], %[c], -4\n\tv_add_u32_e32 %[t1], %[s0], %[lane4]\n\t"
-#define K1R_V2_TAIL                                                                                 \
-    "s_and_b32 %[s1], vcc_lo, 0xffff\n\t"                                                           \
-    "s_cmp_eq_u32 %[s1], 0\n\t"                                                                     \
-    "s_cbranch_scc1 L%=_x4\n\t"                                                                     \
-    "s_ff1_i32_b32 %[s1], %[s1]\n\t"                                                                \
-    "s_nop 1\n\t"                                                                                   \
-    "v_readlane_b32 %[s0], %[t2], %[s1]\n\t"                                                        \
-    "s_sub_u32 %[s1], %[L], %[pf]\n\t"                                                              \
-    "s_min_u32 %[s0], %[s0], %[s1]\n\t"                                                             \
-    "s_cmp_lt_u32 %[s0], 4\n\t"                                                                     \
-    "s_cbranch_scc1 L%=_x5\n\t"                                                                     \
-    "s_add_u32 %[p], %[pf], %[s0]\n\t"                                                              \
-    "s_sub_u32 %[lane0], %[p], %[q0]\n\t"                                                           \
-    "s_lshl_b32 %[s1], %[s0], 16\n\t"                                                               \
-    "s_or_b32 %[dka], %[s1], %[pf]\n\t"                                                             \
-    "s_sub_u32 %[dkb], %[pf], %[c]\n\t"                                                             \
-    "s_mov_b32 %[dkn], 1\n\t"                                                                       \
-    "s_mov_b32 %[skip], 32\n\t"                                                                     \
-    "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                                \
-    "s_cbranch_scc1 L%=_x1\n\t"                                                                     \
-    "s_cmp_le_u32 %[lane0], %[l0max]\n\t"                                                           \
-    "s_cbranch_scc1 L%=_top\n\t"                                                                    \
-    "s_branch L%=_x2\n"
-#endif
-#define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, CAND, SEGHI, WRAP, HIT, PA, LQ)                                    \
+#define K1R_DRAIN                                                                                   \
+    "s_mov_b32 m0, %[pend]\n\t" /* (gfx950 refuses two SGPRs in a v_writelane: m0 stays) */          \
+    "v_writelane_b32 %[tka], %[dka], m0\n\t"                                                        \
+    "v_writelane_b32 %[tkb], %[dkb], m0\n\t"                                                        \
+    "s_add_u32 %[pend], %[pend], %[dkn]\n\t"
+#define K1R_SKIPFIX "s_cmp_eq_u32 %[dkn], 0\n\ts_cselect_b32 %[skip], %[skip], 32\n\t"
+#define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, CAND, SEGHI, HIT)                              \
     do {                                                                                            \
-        uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4, _t5, _t6;                 \
-        (void)_t5;                                                                                  \
-        (void)_t6;                                                                                  \
-        uint64_t _valid, _hm, _wm;                                                                  \
+        uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4;                            \
+        uint64_t _valid, _hm;                                                                       \
         asm volatile(                                                                               \
             "s_mov_b32 %[m0s], m0\n\t"                                                              \
             "s_cmp_gt_u32 %[skip], %[skipmax]\n\t" /* a step of 2 within DMAX probes: C++ round */   \
@@ -1407,56 +885,95 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "L%=_top:\n\t"                                                                          \
             "s_lshl_b64 %[valid], %[dmask], %[lane0]\n\t"                                           \
             "v_cmp_gt_i32_e32 vcc, %[lane0], %[pdl1]\n\t" /* vcc = not in-round */                  \
-            K1R_V6_MWIN_HIT                                                                         \
             "s_waitcnt lgkmcnt(0)\n\t"                                                              \
             HIT                                                                                     \
             "s_and_b64 %[hm], %[hm], %[valid]\n\t"                                                  \
-            K1R_V2_HITBR                                                                            \
+            "s_cbranch_scc0 L%=_nohit\n\t" /* SCC = (hm != 0) */                                     \
             "s_ff1_i32_b64 %[f], %[hm]\n\t"                                                         \
-            PA                                                                                      \
-            K1R_V2_CMASK                                                                            \
+            "v_readlane_b32 %[c], %[t1], %[f]\n\t"                                                  \
+            "s_add_u32 %[pf], %[q0], %[f]\n\t"                                                      \
+            "v_add3_u32 %[t2], %[pf], -1, %[lane4]\n\t" /* dwords from (pf - 1) / 4 */              \
+            "ds_bpermute_b32 %[t2], %[t2], %[dv]\n\t" /* pa: dwords at pf */                        \
             CAND                                                                                    \
-            K1R_V10_PAIR                                                                            \
-            WRAP                                                                                    \
-            K1R_V5_ROT                                                                              \
-            K1R_V15_CA                                                                              \
-            K1R_V5_SEL                                                                              \
+            "s_bfe_u32 %[s1], %[c], 0x60002\n\t"                                                    \
+            "v_cmp_le_u32_e32 vcc, %[s1], %[lane]\n\t" /* lanes >= l0 take register R */           \
+            "v_add_u32_e32 %[t1], %[c], %[lane4]\n\t"                                               \
+            "s_set_gpr_idx_on %[s0], gpr_idx(SRC0,SRC1)\n\t"                                        \
+            "v_cndmask_b32_e32 %[t3], v3, v2, vcc\n\t"                                              \
+            "s_set_gpr_idx_off\n\t"                                                                 \
             "ds_bpermute_b32 %[t3], %[t1], %[t3]\n\t" /* ca: dwords at c */                         \
             "L%=_farret:\n\t"                                                                       \
-            K1R_V6_DRAIN /* the previous round's token, during the gathers */                      \
-            "s_add_u32 %[pend], %[pend], %[dkn]\n\t"                                                \
-            K1R_V5_LO0                                                                              \
-            K1R_V18_PRE                                                                             \
-            K1R_V6_SEL2B                                                                            \
-            K1R_V18_WAIT                                                                            \
+            K1R_DRAIN /* the previous round's token, during the gathers */                         \
+            "s_cmp_lt_u32 %[lane0], %[f]\n\t"                                                       \
+            "s_subb_u32 %[s0], %[lane0], 0\n\t" /* lo0 */                                           \
+            "v_mul_i32_i24_e64 %[t0], %[pf], -8\n\t" /* pa's funnel shift */                        \
+            "s_sub_u32 %[s2], %[f], %[s0]\n\t"                                                      \
+            "s_add_u32 %[s2], %[s2], 1\n\t" /* lanes lo0 .. f insert */                             \
+            "s_and_b32 %[s3], %[c], 3\n\t"                                                          \
+            "s_mul_i32 %[s3], %[s3], 0xfefefeff\n\t"                                                \
+            "s_add_i32 %[s3], %[s3], 0x7060504\n\t" /* ca's perm selector */                        \
+            "s_waitcnt lgkmcnt(0)\n\t" /* pa and ca */                                              \
             "v_mov_b32_dpp %[t1], %[t2] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
             "v_mov_b32_dpp %[t4], %[t3] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
-            K1R_V10_FUNNEL_PA                                                                       \
-            K1R_V11_PERM3                                                                           \
-            K1R_V18_POST                                                                            \
+            "v_alignbit_b32 %[t2], %[t2], %[t1], %[t0]\n\t"                                         \
+            "v_perm_b32 %[t3], %[t3], %[t4], %[s3]\n\t"                                             \
+            "s_bfm_b64 exec, %[s2], %[s0]\n\t"                                                      \
+            "ds_write_b16 %[adr], %[word]\n\t"                                                      \
+            "ds_write_b8_d16_hi %[adrt], %[word] offset:%[tagb]\n\t"                                \
+            "s_mov_b64 exec, -1\n\t"                                                                \
+            "ds_read_u16 %[ent], %[adr]\n\t" /* the next round's entries */                          \
+            "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"                                        \
             "v_cmp_ne_u32_e32 vcc, %[t2], %[t3]\n\t"                                                \
-            K1R_V3_LEN                                                                              \
-            K1R_V2_TAIL                                                                             \
+            "v_xor_b32_e32 %[t2], %[t2], %[t3]\n\t"                                                 \
+            "v_ffbh_u32_e32 %[t2], %[t2]\n\t"                                                       \
+            "v_bfe_u32 %[t2], %[t2], 3, 2\n\t"                                                      \
+            "v_lshl_or_b32 %[t2], %[lane], 2, %[t2]\n\t" /* the prefix length if this dword differs */ \
+            "s_ff1_i32_b32 %[s1], vcc_lo\n\t"                                                       \
+            "s_cmp_gt_u32 %[s1], 15\n\t"                                                            \
+            "s_cbranch_scc1 L%=_x4\n\t"                                                             \
+            "v_readlane_b32 %[s0], %[t2], %[s1]\n\t"                                                \
+            "s_cmp_lt_u32 %[s0], 4\n\t" /* (pf <= L - 16: the clamp below never makes it < 4) */    \
+            "s_cbranch_scc1 L%=_x5\n\t"                                                             \
+            "s_add_u32 %[lane0], %[f], %[s0]\n\t"                                                   \
+            "s_pack_ll_b32_b16 %[dka], %[pf], %[s0]\n\t"                                            \
+            "s_sub_u32 %[dkb], %[pf], %[c]\n\t"                                                     \
+            "s_mov_b32 %[dkn], 1\n\t"                                                               \
+            "s_cmp_le_i32 %[lane0], %[lim0]\n\t" /* implies pf + len <= L - 16: no clamp */         \
+            "s_cbranch_scc1 L%=_top\n\t"                                                            \
+            "s_sub_u32 %[s2], %[L], %[pf]\n\t" /* leaving: the length clamped to the block end */ \
+            "s_min_u32 %[s0], %[s0], %[s2]\n\t"                                                     \
+            "s_add_u32 %[p], %[pf], %[s0]\n\t"                                                      \
+            "s_sub_u32 %[lane0], %[p], %[q0]\n\t"                                                   \
+            "s_lshl_b32 %[s1], %[s0], 16\n\t"                                                       \
+            "s_or_b32 %[dka], %[s1], %[pf]\n\t"                                                     \
+            "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                        \
+            "s_cbranch_scc1 L%=_x1\n\t"                                                             \
+            "s_branch L%=_x2\n"                                                                     \
             "L%=_nohit:\n\t"                                                                        \
-            K1R_V8_SKIPFIX                                                                          \
-            K1R_V6_MWIN_NOHIT                                                                       \
+            K1R_SKIPFIX                                                                             \
+            "s_and_b64 %[valid], %[valid], %[mwin]\n\t"                                             \
             "s_bcnt1_i32_b64 %[s0], %[valid]\n\t" /* nk misses: lanes lane0 - 1 .. lane0 + nk - 1 */ \
-            K1R_V6_DRAIN                                                                            \
-            "s_add_u32 %[pend], %[pend], %[dkn]\n\t"                                                \
+            K1R_DRAIN                                                                               \
             "s_mov_b32 %[dkn], 0\n\t"                                                               \
-            K1R_V9_DKZERO                                                                           \
             "s_add_i32 %[s1], %[lane0], -1\n\t"                                                     \
-            K1R_V13_NOHIT_INSERT                                                                    \
+            "s_add_u32 %[s2], %[skip], %[s0]\n\t"                                                   \
+            "s_add_i32 %[s3], %[s2], -1\n\t"                                                        \
+            "s_add_u32 %[c], %[s0], 1\n\t" /* (c is free on this path) */                          \
+            "s_bfm_b64 exec, %[c], %[s1]\n\t" /* lanes lane0 - 1 .. lane0 - 1 + nk */              \
+            "ds_write_b16 %[adr], %[word]\n\t"                                                      \
+            "ds_write_b8_d16_hi %[adrt], %[word] offset:%[tagb]\n\t"                                \
+            "s_mov_b64 exec, -1\n\t"                                                                \
             "ds_read_u16 %[ent], %[adr]\n\t"                                                        \
             "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"                                        \
             "s_lshr_b32 %[s3], %[s3], 5\n\t" /* the last probe steps by 2 at skip 64 */             \
-            K1R_V9_NOHIT_P                                                                          \
+            "s_add_u32 %[lane0], %[s1], %[s0]\n\t" /* lane0 - 1 + nk + the step-2 probe */          \
+            "s_add_u32 %[lane0], %[lane0], %[s3]\n\t"                                               \
+            "s_add_u32 %[p], %[q0], %[lane0]\n\t"                                                   \
             "s_mov_b32 %[skip], %[s2]\n\t"                                                          \
             "s_cmp_gt_u32 %[skip], %[lsmax]\n\t"                                                    \
             "s_cbranch_scc1 L%=_x1\n\t"                                                             \
             "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                        \
             "s_cbranch_scc1 L%=_x1\n\t"                                                             \
-            K1R_V9_NOHIT_L0                                                                         \
             "s_cmp_gt_u32 %[lane0], %[l0max]\n\t"                                                   \
             "s_cbranch_scc1 L%=_x2\n\t"                                                             \
             "s_cmp_le_u32 %[skip], %[skipmax]\n\t"                                                  \
@@ -1464,25 +981,31 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "L%=_x3:\n\ts_mov_b32 %[code], 3\n\ts_branch L%=_end\n"                                 \
             "L%=_x1:\n\ts_mov_b32 %[code], 1\n\ts_branch L%=_end\n"                                 \
             "L%=_x2:\n\ts_mov_b32 %[code], 2\n\ts_branch L%=_end\n"                                 \
-            "L%=_x4:\n\t" K1R_V18_X4 "s_mov_b32 %[code], 4\n\ts_branch L%=_end\n"                   \
-            K1R_V19_FAR                                                                             \
+            "L%=_x4:\n\ts_mov_b32 %[code], 4\n\ts_branch L%=_end\n"                                 \
+            "L%=_far:\n\t" /* K1r64: the candidate's 256 bytes from the input */                    \
+            "s_and_b32 %[s1], %[c], -4\n\t"                                                         \
+            "v_add_u32_e32 %[t1], %[s1], %[lane4]\n\t"                                              \
+            "global_load_dword %[t3], %[t1], %[srcb]\n\t"                                           \
+            "s_mov_b32 %[s1], 0x10203\n\t"                                                          \
+            "s_waitcnt vmcnt(0)\n\t"                                                                \
+            "v_perm_b32 %[t3], %[t3], %[t3], %[s1]\n\t" /* big-endian, as the ring registers */    \
+            "s_branch L%=_farret\n"                                                                 \
             "L%=_x5:\n\ts_mov_b32 %[code], 5\n"                                                     \
             "L%=_end:\n\t"                                                                          \
-            K1R_V8_SKIPFIX                                                                          \
+            K1R_SKIPFIX                                                                             \
             "s_mov_b32 m0, %[m0s]\n\t"                                                              \
             "s_waitcnt lgkmcnt(0)"                                                                  \
             : [p] "+s"(p), [skip] "+s"(skip), [lane0] "+s"(lane0), [pend] "+s"(pend), [dka] "+s"(dka), \
               [dkb] "+s"(dkb), [dkn] "+s"(dkn), [code] "=&s"(code), [f] "=&s"(fx), [c] "=&s"(cx),      \
               [m0s] "=&s"(_m0s), [pf] "=&s"(_pf), [s0] "=&s"(_s0), [s1] "=&s"(_s1), [s2] "=&s"(_s2),   \
-              [s3] "=&s"(_s3), [valid] "=&s"(_valid), [hm] "=&s"(_hm), [wm] "=&s"(_wm), [ent] "+v"(e32), \
+              [s3] "=&s"(_s3), [valid] "=&s"(_valid), [hm] "=&s"(_hm), [ent] "+v"(e32),                \
               [entt] "+v"(et32), [tka] "+v"(tka), [tkb] "+v"(tkb), [t0] "=&v"(_t0), [t1] "=&v"(_t1),  \
-              [t2] "=&v"(_t2), [t3] "=&v"(_t3), [t4] "=&v"(_t4) K1R_V11_OUTS                          \
+              [t2] "=&v"(_t2), [t3] "=&v"(_t3), [t4] "=&v"(_t4)                                        \
             : [q0] "s"(q0), [L] "s"(L), [lm16] "s"(L - 16), [mwin] "s"(m_win), [seghi] SEGHI,         \
               [lim0] "s"(__builtin_elementwise_min((int32_t)(62 - SNAPPY_K1R_RMIN), (int32_t)L - 16 - (int32_t)q0)), \
-              [pdz] "s"(m_pdz),                                                                     \
               [dv] "v"(dv),                                                                         \
               [pdl1] "v"(pdl1), [pdc] "v"(pdc), [pdnz] "v"(pdnz), [adr] "v"(adr), [adrt] "v"(adr >> 1), \
-              [word] "v"(word), [lane] "v"(lane), [lane4] "v"(lane << 2) K1R_V13_DUMMY_IN, [srcb] "s"(src), [lq] "v"(LQ),         \
+              [word] "v"(word), [lane] "v"(lane), [lane4] "v"(lane << 2), [srcb] "s"(src),            \
               [skipmax] "i"(64 - DMAX), [dmask] "i"((1u << DMAX) - 1), [lsmax] "i"(64 - SNAPPY_K1R_LSMIN), \
               [l0max] "i"(62 - SNAPPY_K1R_RMIN), [tagb] "i"(kTagBase), "{v[2:33]}"(g0), "{v[34:65]}"(g1), \
               "{v[66:97]}"(g2), "{v[98:129]}"(g3)                                                      \
@@ -1566,7 +1089,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             if (!went) TBL_READ_ENT(adr);
             for (;;) {
 #if K1R_ASM_ROUNDS
-                if constexpr (!BIG || SNAPPY_K1R_ASM_BIG) {
+                {
                     // the common rounds as one hand-scheduled loop (k1r_asm_rounds below)
                     uint32_t code, fx, cx;
                     uint32_t e32 = ent, et32 = ent_t;
@@ -1575,11 +1098,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     RSTAMP(ra0);
 #endif
                     if constexpr (BIG)
-                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND64, K1R_SEGHI64(seg_hi), K1R_WRAP64,
-                                            K1R_HIT64, K1R_PA64, lane << 2);
+                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND64, K1R_SEGHI64(seg_hi), K1R_HIT64);
                     else
-                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND32, "i"(0), "", K1R_HIT32, K1R_PA32,
-                                            K1R_LQ32);
+                        K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, K1R_CAND32, "i"(0), K1R_HIT32);
 #ifdef SNAPPY_K1R_RSTAMPS
                     RSTAMP(ra1);
                     rs_asm += ra1 - ra0;

@@ -357,10 +357,11 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
 // with the lane's (16-bit field: a lane past the window has bit 24 of its word
 // set and never matches) -- two VALU instead of three.  1 = both kernels, 2 =
 // K1r64 only (A/B, profiles/r05za_*: 64 KiB blocks 15.04-15.08 -> 14.51 ms per
-// GiB, 32 KiB streams 12.89 -> 13.04: the same three instructions fewer measure
-// differently in the two kernels' schedules)
+// GiB; 32 KiB streams 12.89 -> 13.04 there, but with the loop's placement pinned
+// at its best offset for each build 12.56 -> 12.34-12.36, profiles/r05zs_*: the
+// first K1r figure was a placement effect)
 #ifndef SNAPPY_K1R_ASM_V16
-#define SNAPPY_K1R_ASM_V16 2
+#define SNAPPY_K1R_ASM_V16 1
 #endif
 template <bool BIG>
 __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
@@ -653,7 +654,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             REG_PAIR(d0 >> 6, _r0, _r1);                                                           \
             dv = lane >= dr ? _r0 : _r1;                                                           \
         }                                                                                          \
-        if (SNAPPY_K1R_WIN_ALIGN && !BIG) {                                                        \
+        if (SNAPPY_K1R_WIN_ALIGN == 2 || (SNAPPY_K1R_WIN_ALIGN && !BIG)) { \
             /* the dwords from (p - 1) / 4 funnelled by v_alignbit with the lane's */              \
             /* shift -8 p (bits 4:0; 0 takes the second dword, the one at p) */                    \
             const uint32_t _p = q0 + lane;                                                          \
@@ -809,9 +810,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 // of 64 KiB blocks each, outputs checked identical; DESIGN.md 4.2 lists them, the
 // logs are profiles/r05e_* .. r05zk_*).  What stayed, in the order the round runs:
 //  * the hit test: the candidate of every lane (in-window predecessor or table
-//    entry) and its tag compared in one SDWA compare (K1r64: the lane data carry
-//    the predecessor's tag, V16; K1r keeps the tag-difference select, which
-//    measured faster in its schedule); a lane past the window has bit 24 of its
+//    entry) and its tag compared in one SDWA compare (the lane data carry the
+//    predecessor's tag, V16); a lane past the window has bit 24 of its
 //    word set, so it never matches (V6); the hit branch on the SCC of the s_and
 //    that makes the hit mask (V2)
 //  * pa: the dwords at pf gathered from (pf - 1) / 4 and funnelled by v_alignbit
@@ -841,7 +841,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 // left to the code around the statement.  The padding (s_nop) runs once per
 // entry into the asm loop.
 #ifndef SNAPPY_K1R_PAD32
-#define SNAPPY_K1R_PAD32 3
+#define SNAPPY_K1R_PAD32 2
 #endif
 #ifndef SNAPPY_K1R_PAD64
 #define SNAPPY_K1R_PAD64 -1

@@ -53,6 +53,9 @@ struct snappy_amd_ctx {
 // grow a device buffer to at least `need` bytes (contents not kept); the slack
 // is capped (dist.py's _grown mirrors it for bench.py's memory plan)
 SNAPPY_PRIVATE int grow(void **ptr, size_t *cap, size_t need);
+// c->stream, creating the context's own stream if none is bound and none was
+// made yet (contexts create it lazily: a caller-bound stream leaves no idle one)
+SNAPPY_PRIVATE int ctx_stream(snappy_amd_ctx *c);
 // K1r (or K1r64) -> K3 -> K2 on c->stream; *out_len (when non-null) after a
 // sync of that stream, otherwise the size stays in c->total (device)
 extern "C" SNAPPY_PRIVATE int compress_impl(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t chunk, int layout,

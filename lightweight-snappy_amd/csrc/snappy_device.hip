@@ -31,6 +31,20 @@ int grow(void **ptr, size_t *cap, size_t need)
     return SNAPPY_AMD_OK;
 }
 
+int ctx_stream(snappy_amd_ctx *c)
+{
+    if (c->stream) return SNAPPY_AMD_OK;
+    // a blocking stream: work a caller queued on the legacy default stream (torch's
+    // default stream, cuda_stream == 0, which set_stream(NULL) maps here) is
+    // ordered before the context's launches (a non-blocking own stream raced it)
+    if (!c->own) {
+        HIP_OK(hipSetDevice(c->device));
+        HIP_OK(hipStreamCreateWithFlags(&c->own, hipStreamDefault));
+    }
+    c->stream = c->own;
+    return SNAPPY_AMD_OK;
+}
+
 extern "C" {
 
 int snappy_amd_create(int device, snappy_amd_ctx **out)
@@ -43,11 +57,9 @@ int snappy_amd_create(int device, snappy_amd_ctx **out)
     HIP_OK(hipSetDevice(device));
     snappy_amd_ctx *c = new snappy_amd_ctx();
     c->device = device;
-    // a blocking stream: work a caller queued on the legacy default stream (torch's
-    // default stream, cuda_stream == 0, which set_stream(NULL) maps here) is
-    // ordered before the context's launches (a non-blocking own stream raced it)
-    if (hipStreamCreateWithFlags(&c->own, hipStreamDefault) != hipSuccess) { delete c; return SNAPPY_AMD_ERR_DEVICE; }
-    c->stream = c->own;
+    // the context's own stream is created on first use (ctx_stream), so a context
+    // whose caller binds a stream of its own never holds an idle one (DESIGN.md 6:
+    // the streams of a rank at N > 1 against GPU_MAX_HW_QUEUES)
     if (hipMalloc(&c->total, 64) != hipSuccess || hipMalloc(&c->k5res, 64) != hipSuccess ||
         hipHostMalloc(&c->h_total, 64, hipHostMallocDefault) != hipSuccess) {
         snappy_amd_destroy(c);
@@ -123,11 +135,11 @@ int snappy_amd_set_option(snappy_amd_ctx *c, int option, int64_t value)
 int snappy_amd_set_stream(snappy_amd_ctx *c, void *s)
 {
     if (!c) return SNAPPY_AMD_ERR_ARG;
-    c->stream = s ? static_cast<hipStream_t>(s) : c->own;
+    c->stream = s ? static_cast<hipStream_t>(s) : c->own;  // (own: created at the next use if none yet)
     return SNAPPY_AMD_OK;
 }
 
-void *snappy_amd_get_stream(snappy_amd_ctx *c) { return c ? c->stream : nullptr; }
+void *snappy_amd_get_stream(snappy_amd_ctx *c) { return c && ctx_stream(c) == SNAPPY_AMD_OK ? c->stream : nullptr; }
 
 int snappy_amd_enable_timing(snappy_amd_ctx *c, int on)
 {
@@ -186,6 +198,7 @@ int compress_impl(snappy_amd_ctx *c, const void *d_in, size_t n, uint32_t chunk,
     const uint32_t unit = layout == SNAPPY_AMD_SINGLE ? SNAPPY_AMD_BLOCK : chunk;
     if (unit == 0 || unit > SNAPPY_AMD_BLOCK) return SNAPPY_AMD_ERR_ARG;
     HIP_OK(hipSetDevice(c->device));
+    if (ctx_stream(c)) return SNAPPY_AMD_ERR_DEVICE;
     if (n == 0) {
         // src/snappy_compression.c:417-421: no block, so no header either
         HIP_OK(hipMemsetAsync(d_offsets, 0, sizeof(uint64_t), c->stream));
@@ -272,6 +285,7 @@ static int decompress_launch(snappy_amd_ctx *c, const void *d_comp, const uint64
     const uint32_t unit = layout == SNAPPY_AMD_SINGLE ? SNAPPY_AMD_BLOCK : chunk;
     if (unit == 0 || unit > SNAPPY_AMD_BLOCK) return SNAPPY_AMD_ERR_ARG;
     HIP_OK(hipSetDevice(c->device));
+    if (ctx_stream(c)) return SNAPPY_AMD_ERR_DEVICE;
     c->last_units = 0;
     c->status_pending = false;
     c->last_status = SNAPPY_AMD_OK;
@@ -369,6 +383,7 @@ int snappy_amd_index_device(snappy_amd_ctx *c, const void *d_comp, size_t clen, 
 {
     if (!c || !d_comp || !d_offsets) return SNAPPY_AMD_ERR_ARG;
     HIP_OK(hipSetDevice(c->device));
+    if (ctx_stream(c)) return SNAPPY_AMD_ERR_DEVICE;
     (void)hipGetLastError();  // (a pending error that is not this launch's, as in compress_impl)
     const uint8_t *comp = static_cast<const uint8_t *>(d_comp);
     const bool serial = c->serial_index;

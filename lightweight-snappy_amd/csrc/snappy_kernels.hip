@@ -270,12 +270,11 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
 }
 
 #ifndef SNAPPY_K1R_DMAX
-#define SNAPPY_K1R_DMAX 9  // lane-space rounds: same-hash distances resolved per window (8/10/12/14/16
-                           // measured, profiles/r03h_ab_k1r_dmax_rmin_*; after the early entry read
-                           // 9 / 10 / 12: 16.07 / 16.19 / 16.18 ms per GiB, profiles/r03s2z_*, r03s2aa_*;
-                           // with the round-5 asm loop, each at its best loop placement, 8 / 9 / 10:
-                           // 12.46 / 12.37 / 12.23 ms per GiB, profiles/r05zw_*; 10 waits for a GPU
-                           // test run of its own)
+#define SNAPPY_K1R_DMAX 10  // lane-space rounds: same-hash distances resolved per window (8/10/12/14/16
+                            // measured, profiles/r03h_ab_k1r_dmax_rmin_*; after the early entry read
+                            // 9 / 10 / 12: 16.07 / 16.19 / 16.18 ms per GiB, profiles/r03s2z_*, r03s2aa_*;
+                            // with the round-5 asm loop, each at its best loop placement, 8 / 9 / 10:
+                            // 12.46 / 12.37 / 12.23 ms per GiB, profiles/r05zw_*)
 #endif
 #ifndef SNAPPY_K1R_DMAX64
 #define SNAPPY_K1R_DMAX64 9  // K1r64 (65,536-byte blocks), with the asm round loop: 9 / 10 / 11 / 12 -> 18.70-18.73 / 18.81-18.82 / 18.75 / 18.81-18.84 ms

@@ -42,6 +42,19 @@ extern "C" {
 // reads chunk k+1.  Chunk 0 carries the varint(header_value) preamble, the
 // others are compressed with it suppressed.
 namespace {
+// a host pipeline's context: its own stream made at once (the pipelines copy on
+// c->stream before the first launch; device-API contexts create theirs lazily)
+int create_host_ctx(int device, snappy_amd_ctx **out)
+{
+    int rc = snappy_amd_create(device, out);
+    if (rc) return rc;
+    if ((rc = ctx_stream(*out))) {
+        snappy_amd_destroy(*out);
+        *out = nullptr;
+    }
+    return rc;
+}
+
 // A pipeline context's own stream at high priority: high-priority streams take
 // hardware queues of their own, where default-priority streams share the
 // process's few (GPU_MAX_HW_QUEUES, 4 by default) with the caller's streams,
@@ -373,7 +386,7 @@ void slot_free(StreamSlot &s)
 int slot_init(StreamSlot &s, int device)
 {
     if (s.c) return SNAPPY_AMD_OK;
-    int rc = snappy_amd_create(device, &s.c);
+    int rc = create_host_ctx(device, &s.c);
     if (rc) return rc;
     const size_t maxo = snappy_amd_max_output(kStreamChunk, SNAPPY_AMD_BLOCK, SNAPPY_AMD_SINGLE);
     const size_t units = kStreamChunk / SNAPPY_AMD_BLOCK;
@@ -543,7 +556,7 @@ public:
         if (!h_) {
             HostCtx *h = new HostCtx();
             h->device = device;
-            rc_ = snappy_amd_create(device, &h->c);
+            rc_ = create_host_ctx(device, &h->c);
             if (rc_) delete h;
             else h_ = h;
         }
@@ -669,7 +682,7 @@ int host_compress_pipelined(HostCtx &h, const uint8_t *in, size_t n, uint64_t he
     h.pipe[0] = h.c;
     for (int i = 1; i < lanes; i++)
         if (!h.pipe[i]) {
-            if ((rc = snappy_amd_create(h.device, &h.pipe[i]))) {
+            if ((rc = create_host_ctx(h.device, &h.pipe[i]))) {
                 h.pipe[i] = nullptr;
                 return rc;
             }

@@ -753,6 +753,9 @@ def resolve_sizes(args, world: int, rank: int):
             n = DECODE10G_BYTES
         total = n * world
     e2e = piece_step(unit, args.e2e_piece_bytes) if args.e2e_piece_bytes else default_e2e_piece(total, world, unit)
+    # a piece larger than the whole job is the job (dist.rank_plan sizes the
+    # payload slot from the same bound, so the allocations match the plan)
+    e2e = min(e2e, piece_step(unit, total + unit - 1))
     gp = piece_plan(total, world, rank, unit, e2e)
     return strong, total, gp, sum(m for _, _, m in gp), e2e, pipeline_steps(total, world, unit, e2e)
 
@@ -979,9 +982,12 @@ def end_to_end(job: Job, world: int, rank: int, args, cdev, gloo, allgather, tot
         dist.all_gather(parts, t, group=meta)
         return [int(v) for v in parts]
 
-    def run():
+    statuses = []  # (verification run) each step's decode status
+
+    def run(verify=False):
         base = 0
         sizes_log.clear()
+        statuses.clear()
         for k in range(steps_k):
             gp = job.gpieces[k] if k < len(job.gpieces) else None
             clen = 0
@@ -1000,6 +1006,8 @@ def end_to_end(job: Job, world: int, rank: int, args, cdev, gloo, allgather, tot
                 dcodec.decompress_ptr_ex(stream.data_ptr() + base + int(sum(sz[:rank])), gp.offs.data_ptr(), gp.n,
                                          chunk, layout, gp.flags, job.header_value, job.back.data_ptr() + gp.xoff,
                                          check=False)
+                if verify:  # (waits for this step's decode: the verification run only)
+                    statuses.append(dcodec.decompress_status())
             if not overlap:
                 torch.cuda.synchronize(dev)
             base += sum(sz)
@@ -1021,8 +1029,13 @@ def end_to_end(job: Job, world: int, rank: int, args, cdev, gloo, allgather, tot
     torch_peak = torch.cuda.max_memory_allocated(dev)  # before the checks' temporaries
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     t = float(tt) / runs
-    st = dcodec.decompress_status()
-    ok = st == 0 and all(bool(torch.equal(job.back[o:min(o + GiB, job.n)], job.x[o:min(o + GiB, job.n)]))
+    # verification: one more (untimed) run into a poisoned output, every step's
+    # decode status read -- the timed runs' output cannot vouch for itself
+    job.back.fill_(0xA5)
+    torch.cuda.synchronize(dev)
+    total_stream = run(verify=True)
+    st = next((v for v in statuses if v != 0), 0)
+    ok = st == 0 and len(statuses) == len(job.gpieces) and all(bool(torch.equal(job.back[o:min(o + GiB, job.n)], job.x[o:min(o + GiB, job.n)]))
                          for o in range(0, job.n, GiB))
     # every global piece: its owner's payload checksum against its run of this rank's stream
     mine = [checksum(job.out[gp.k * job.slot:gp.k * job.slot + gp.clen]) for gp in job.gpieces]

@@ -11,7 +11,9 @@
  *
  * Added below them: an in-memory host-buffer API and a
  * device-resident (HBM pointer) batch API.  All compute runs in hand-written
- * HIP kernels for gfx950; there is no CPU fallback in this library.  Every
+ * HIP kernels for gfx950; there is no CPU fallback in this library.  (The
+ * reference's -b BST compressor, a different algorithm with different output
+ * and not the GPU path, runs on host threads: snappy_compress_bst.)  Every
  * function returns 0 (SNAPPY_AMD_OK) or a negative error code.
  */
 #ifndef SNAPPY_AMD_H
@@ -49,11 +51,19 @@ extern "C" {
 /* ---- drop-in FILE* API (reference signatures) ------------------------ */
 void snappy_compress(FILE *file_input, unsigned long long input_size, FILE *file_compressed);
 int snappy_decompress(FILE *file_input, FILE *file_decompressed);
+/* the -b mode: the reference's BST-matcher stream, byte for byte, computed by
+ * a pool of host threads (<= 16, SNAPPY_AMD_BST_THREADS), one block each */
 int snappy_compress_bst(FILE *file_input, unsigned long long input_size, FILE *file_compressed);
 
 /* Status of the last snappy_compress / snappy_decompress call on this
  * thread (the reference signatures cannot return one). */
 int snappy_amd_last_status(void);
+
+/* The compile-time knobs of the library's gfx950 kernels, e.g.
+ * "compress{measurement=0 k1r_dmax=10 ...} decode{measurement=0 k4_nofar=0 ...}".
+ * measurement=1 marks a build that may write wrong bytes (timing experiments)
+ * or carries statistics code: never a product library. */
+const char *snappy_amd_build_config(void);
 
 /* Sidecar block index (the stream format has no block
  * markers).  File layout, little-endian u64 words: SNAPPY_AMD_IDX_MAGIC, N
@@ -88,6 +98,10 @@ size_t snappy_max_compressed_length(size_t n);
 /* Same bytes as snappy_compress() on a FILE holding in[0..n); n == 0 gives
  * 0 bytes.  out must hold snappy_max_compressed_length(n). */
 int snappy_compress_buffer(const uint8_t *in, size_t n, uint8_t *out, size_t *out_len);
+/* Same bytes as snappy_compress_bst() on a FILE holding in[0..n) (the -b
+ * stream; snappy_decompress_buffer decodes it).  out must hold
+ * snappy_max_compressed_length(n); n == 0 gives 0 bytes. */
+int snappy_compress_bst_buffer(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len);
 /* Decode one stream; *out_len = declared length. */
 int snappy_decompress_buffer(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len);
 int snappy_uncompressed_length(const uint8_t *in, size_t n, uint64_t *len);

@@ -1,7 +1,8 @@
 /*
- * snappy_amd_internal.h -- host-buffer entry points of the HIP shim
- * (snappy_device.hip) that the C host layer (snappy_host.c) builds the
- * reference FILE* API on.  Exported for the host layer; not part of the
+ * snappy_amd_internal.h -- host-buffer and FILE* entry points of the host
+ * pipelines (snappy_pipeline.cpp, over the HIP shim snappy_device.hip) and of
+ * the -b compressor (bst_host.c) that the C host layer (snappy_host.c) builds
+ * the reference FILE* API on.  Exported for the host layer; not part of the
  * documented drop-in surface.
  */
 #ifndef SNAPPY_AMD_INTERNAL_H
@@ -35,6 +36,9 @@ int snappy_amd_host_compress_file(FILE *fin, uint64_t header_value, FILE *fout, 
  * SNAPPY_AMD_ERR_UNSUPPORTED if fin is not a regular file (the caller then
  * reads it whole and uses snappy_amd_host_decompress[_idx]). */
 int snappy_amd_host_decompress_file(FILE *fin, const uint64_t *idx, size_t count, FILE *fout);
+/* snappy_compress_bst's stream: fin from its current position to EOF,
+ * varint(header_value) ++ the BST-matcher blocks to fout (bst_host.c) */
+int snappy_amd_bst_compress_file(FILE *fin, uint64_t header_value, FILE *fout);
 #ifdef __cplusplus
 }
 #endif

@@ -47,6 +47,20 @@ int ctx_stream(snappy_amd_ctx *c)
 
 extern "C" {
 
+const char *snappy_amd_config_compress(void);
+const char *snappy_amd_config_decode(void);
+
+const char *snappy_amd_build_config(void)
+{
+    static char cfg[512];
+    static int made = 0;
+    if (!made) {  // (the same bytes from every thread that races here)
+        snprintf(cfg, sizeof cfg, "%s %s", snappy_amd_config_compress(), snappy_amd_config_decode());
+        made = 1;
+    }
+    return cfg;
+}
+
 int snappy_amd_create(int device, snappy_amd_ctx **out)
 {
     if (!out) return SNAPPY_AMD_ERR_ARG;

@@ -1,8 +1,9 @@
 /*
  * snappy_host.c -- C host layer of the MI355X Snappy codec: the reference's
  * FILE* entry points, the varint preamble and the host-buffer API, built on
- * the HIP shim (snappy_device.hip).  No compression or decompression runs on
- * the CPU here: every byte goes through the gfx950 kernels.
+ * the HIP shim (snappy_device.hip).  No compression or decompression of the
+ * GPU path runs on the CPU here: every byte goes through the gfx950 kernels
+ * (the -b BST mode, a different algorithm, is bst_host.c's host threads).
  *
  * Reference interfaces replaced (tturturiello/lightweight-snappy):
  *   snappy_compress      src/snappy_compression.h:8, .c:414-428
@@ -180,11 +181,12 @@ int snappy_compress_file_indexed(FILE *file_input, unsigned long long input_size
 
 int snappy_compress_bst(FILE *file_input, unsigned long long input_size, FILE *file_compressed)
 {
-    (void)file_input;
-    (void)input_size;
-    (void)file_compressed;
-    fprintf(stderr, "snappy_compress_bst: the -b BST matcher is not part of the MI355X codec\n");
-    g_last_status = SNAPPY_AMD_ERR_UNSUPPORTED;
-    return SNAPPY_AMD_ERR_UNSUPPORTED;
+    /* the reference's -b stream (snappy_compression_tree.c:291-306), host threads
+     * (bst_host.c); header = the caller's input_size, an empty read writes nothing */
+    int rc = (file_input && file_compressed)
+                 ? snappy_amd_bst_compress_file(file_input, (uint64_t)input_size, file_compressed)
+                 : SNAPPY_AMD_ERR_ARG;
+    g_last_status = rc;
+    if (rc != SNAPPY_AMD_OK) fprintf(stderr, "snappy_compress_bst: error %d\n", rc);
+    return rc;
 }
-

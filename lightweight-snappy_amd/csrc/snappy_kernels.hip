@@ -30,6 +30,14 @@
 #define SNAPPY_TU_COMPRESS (SNAPPY_TU != 2)
 #define SNAPPY_TU_DECODE (SNAPPY_TU != 1)
 
+// Measurement-only knobs whose kernels write WRONG bytes (they time what a
+// piece of work costs by skipping it): a product build cannot set them.  The
+// shipped library reports its knobs through snappy_amd_build_config(), which
+// tests/test_abi.py and the GPU tests check.
+#if ((defined(SNAPPY_K2_NOLIT) && SNAPPY_K2_NOLIT) || defined(SNAPPY_K4_NOFAR)) && !defined(SNAPPY_MEASUREMENT_BUILD)
+#error "SNAPPY_K2_NOLIT / SNAPPY_K4_NOFAR write wrong output: measurement builds only (-DSNAPPY_MEASUREMENT_BUILD)"
+#endif
+
 namespace snappy_amd {
 
 // v_writelane_b32 (no clang builtin in this toolchain): the LLVM intrinsic by name
@@ -3846,6 +3854,43 @@ __global__ __launch_bounds__(64) void k5d_result(uint32_t nchunks, const int32_t
 #endif
 
 }  // namespace snappy_amd
+
+// The knobs this object was built with (snappy_amd_build_config in
+// snappy_device.hip joins the two halves): measurement = a build that may write
+// wrong output or carries statistics / timestamp code, 0 for the product.
+#define CFG_STR2(x) #x
+#define CFG_STR(x) CFG_STR2(x)
+#if defined(SNAPPY_MEASUREMENT_BUILD) || defined(SNAPPY_K4_NOFAR) || (defined(SNAPPY_K2_NOLIT) && SNAPPY_K2_NOLIT) || \
+    defined(SNAPPY_K1R_STATS) || defined(SNAPPY_K1R_LSTAMPS) || defined(SNAPPY_K1R_RSTAMPS) || defined(SNAPPY_K4_STATS)
+#define CFG_MEASURE "1"
+#else
+#define CFG_MEASURE "0"
+#endif
+#if SNAPPY_TU_COMPRESS
+extern "C" __attribute__((visibility("hidden"))) const char *snappy_amd_config_compress(void)
+{
+    return "compress{measurement=" CFG_MEASURE " k1r_dmax=" CFG_STR(SNAPPY_K1R_DMAX) " k1r_dmax64=" CFG_STR(
+        SNAPPY_K1R_DMAX64) " k1r_rmin=" CFG_STR(SNAPPY_K1R_RMIN) " k1r_pad32=" CFG_STR(SNAPPY_K1R_PAD32) " k1r_pad64=" CFG_STR(SNAPPY_K1R_PAD64)
+#if K1R_ASM_ROUNDS
+           " k1r_asm=1"
+#else
+           " k1r_asm=0"
+#endif
+           " k2_nolit=" CFG_STR(SNAPPY_K2_NOLIT) " k2_pass=" CFG_STR(SNAPPY_K2_PASS) "}";
+}
+#endif
+#if SNAPPY_TU_DECODE
+extern "C" __attribute__((visibility("hidden"))) const char *snappy_amd_config_decode(void)
+{
+    return "decode{measurement=" CFG_MEASURE
+#ifdef SNAPPY_K4_NOFAR
+           " k4_nofar=1"
+#else
+           " k4_nofar=0"
+#endif
+           " k4_bpl4=" CFG_STR(SNAPPY_K4_BPL4) " k4_pass_pipe=" CFG_STR(SNAPPY_K4_PASS_PIPE) "}";
+}
+#endif
 
 #if defined(SNAPPY_K4_STATS) && SNAPPY_TU_DECODE
 extern "C" int snappy_amd_debug_k4_stats(uint64_t *host, size_t count)

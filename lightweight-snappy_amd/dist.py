@@ -129,6 +129,7 @@ def rank_plan(total: int, world: int, unit: int, piece_bytes: int, exchange: boo
     `gather_decoded` (C3, opt-in) runs after the codec scratch and C2 buffers
     are released: every rank then also holds world x the largest shard."""
     e2e = piece_step(unit, e2e_piece or default_e2e_piece(total, world, unit))
+    e2e = min(e2e, piece_step(unit, total + unit - 1))  # (as bench.resolve_sizes: at most the job)
     shard = max(sum(n for _, _, n in piece_plan(total, world, r, unit, e2e)) for r in range(world))
     ps = pieces_of(shard, unit, piece_bytes)
     big = max(ps + [min(e2e, total)]) if ps else 0

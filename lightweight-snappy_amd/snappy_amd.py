@@ -71,6 +71,10 @@ _SIGS = {
     "snappy_varint_decode": (_c.c_uint32, [_c.c_void_p, _c.c_size_t, _c.POINTER(_c.c_uint64)]),
     "snappy_max_compressed_length": (_c.c_size_t, [_c.c_size_t]),
     "snappy_compress_buffer": (_c.c_int, [_c.c_void_p, _c.c_size_t, _c.c_void_p, _c.POINTER(_c.c_size_t)]),
+    "snappy_amd_build_config": (_c.c_char_p, []),
+    "snappy_amd_bst_compress_file": (_c.c_int, [_c.c_void_p, _c.c_uint64, _c.c_void_p]),
+    "snappy_compress_bst_buffer": (_c.c_int, [_c.c_void_p, _c.c_size_t, _c.c_void_p, _c.c_size_t,
+                                              _c.POINTER(_c.c_size_t)]),
     "snappy_decompress_buffer": (_c.c_int, [_c.c_void_p, _c.c_size_t, _c.c_void_p, _c.c_size_t,
                                             _c.POINTER(_c.c_size_t)]),
     "snappy_uncompressed_length": (_c.c_int, [_c.c_void_p, _c.c_size_t, _c.POINTER(_c.c_uint64)]),
@@ -183,6 +187,12 @@ def _buf(data) -> Tuple[ctypes.c_void_p, int, object]:
     return ctypes.cast(keep, ctypes.c_void_p), n, keep
 
 
+def build_config() -> str:
+    """The kernels' compile-time knobs (snappy_amd_build_config); a product
+    library reports measurement=0 for both halves."""
+    return lib().snappy_amd_build_config().decode()
+
+
 # ---- varint (src/varint.c) ------------------------------------------------
 def varint_encode(n: int) -> bytes:
     out = ctypes.create_string_buffer(16)
@@ -211,6 +221,17 @@ def compress(data, header_value: Optional[int] = None) -> bytes:
     got = ctypes.c_size_t(0)
     hv = n if header_value is None else header_value
     _check(lib().snappy_amd_host_compress(p, n, hv, out, cap, ctypes.byref(got)), "compress")
+    return out.raw[: got.value]
+
+
+def compress_bst(data) -> bytes:
+    """The -b stream, byte-identical to the reference snappy_compress_bst()
+    (src/snappy_compression_tree.c:291-306): host threads, no GPU."""
+    p, n, keep = _buf(data)
+    cap = max_compressed_length(n)
+    out = ctypes.create_string_buffer(max(cap, 1))
+    got = ctypes.c_size_t(0)
+    _check(lib().snappy_compress_bst_buffer(p, n, out, cap, ctypes.byref(got)), "compress_bst")
     return out.raw[: got.value]
 
 

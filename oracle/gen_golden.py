@@ -15,7 +15,12 @@ Entries:
     copies into earlier blocks; hand-built and seeded random foreign streams);
   * the reference's own varint KATs (src/test_varint.c:27-35);
   * the 32 KiB-stream layout of BASELINE.json configs[1] on a 32 MiB sample.
-Usage: python oracle/gen_golden.py
+`python oracle/gen_golden.py bst` writes tests/golden/golden_bst.json instead:
+the reference's -b compressor (snappy_compress_bst,
+src/snappy_compression_tree.c:291-306) over the same Appendix A.4 edge matrix,
+period sweep and larger pins, each output checked to round-trip through the
+reference decoder.
+Usage: python oracle/gen_golden.py [bst]
 """
 from __future__ import annotations
 
@@ -73,6 +78,56 @@ def entry(name: str, spec: dict, data: bytes | None = None) -> dict:
     return e
 
 
+EDGE_SIZES = [1, 2, 3, 4, 5, 15, 16, 17, 18, 31, 32, 33, 59, 60, 61, 63, 64, 65, 255, 256, 257, 511, 512, 1025,
+              2048, 2049, 4095, 4096, 4097, 32767, 32768, 32769, 65535, 65536, 65537, 131072, 131073]
+EDGE_KINDS = [("T", {"seed": 7}), ("R", {"seed": 3}), ("Z", {}), ("P", {"seed": 2})]
+PERIODS = [1, 2, 3, 4, 5, 7, 11, 12, 13, 63, 64, 65, 67, 68, 69, 2047, 2048, 2049, 3000]
+
+
+def bst_entry(name: str, spec: dict) -> dict:
+    data = make_input(spec)
+    out = oracle.ref_compress_bst(data)
+    dec = oracle.ref_decompress(out, len(data)) if data else b""
+    assert dec == data, f"reference -b round trip failed on {name}"
+    e = {"name": name, "spec": spec, "in_len": len(data), "in_sha256": sha(data), "out_len": len(out),
+         "out_sha256": sha(out)}
+    if len(out) <= HEX_LIMIT:
+        e["out_hex"] = out.hex()
+    else:
+        e["out_prefix_hex"] = out[:64].hex()
+    return e
+
+
+def main_bst() -> None:
+    entries = []
+    for name, spec in [("abc", {"kind": "bytes", "size": 3, "hex": b"abc".hex()}),
+                       ("a_x20", {"kind": "bytes", "size": 20, "hex": (b"a" * 20).hex()}),
+                       ("hello", {"kind": "bytes", "size": 16, "hex": b"Hello, Snappy!!!".hex()}),
+                       ("empty", {"kind": "bytes", "size": 0, "hex": ""}),
+                       ("license", {"kind": "license", "size": 1069}),
+                       ("license_1MiB", {"kind": "license", "size": 1 << 20}),
+                       ("zeros_1MiB", {"kind": "Z", "size": 1 << 20}),
+                       ("iota64_1MiB", {"kind": "iota64", "size": 1 << 20})]:
+        entries.append(bst_entry(name, spec))
+    for k, extra in EDGE_KINDS:
+        for n in EDGE_SIZES:
+            entries.append(bst_entry(f"edge_{k}_{n}", {"kind": k, "size": n, **extra}))
+    for period in PERIODS:
+        for n in [200, 5000, 65536, 70000]:
+            entries.append(bst_entry(f"period_{period}_{n}", {"kind": "K", "size": n, "seed": 100 + period,
+                                                             "period": period}))
+    entries.append(bst_entry("text_1000000", {"kind": "T", "size": 1000000, "seed": 1234}))
+    entries.append(bst_entry("text_3MiB", {"kind": "T", "size": 3 << 20, "seed": 99}))
+    entries.append(bst_entry("random_1MiB", {"kind": "R", "size": 1 << 20, "seed": 1}))
+    entries.append(bst_entry("repeat_1MiB", {"kind": "P", "size": 1 << 20, "seed": 2}))
+    entries.append(bst_entry("lcg1_1MiB", {"kind": "L", "size": 1 << 20, "seed": 1}))
+    gold = {"generator": "oracle/gen_golden.py bst", "reference": "tturturiello/lightweight-snappy (oracle/_ref, "
+            "snappy_compress_bst)", "entries": entries}
+    with open(os.path.join(GOLD, "golden_bst.json"), "w") as f:
+        json.dump(gold, f, indent=1)
+    print(f"wrote {len(entries)} -b entries")
+
+
 def main() -> None:
     os.makedirs(GOLD, exist_ok=True)
     shutil.copyfile("/root/reference/LICENSE", os.path.join(GOLD, "license.bin"))
@@ -93,14 +148,11 @@ def main() -> None:
     for name, spec in kat:
         entries.append(entry(name, spec))
     # --- Appendix A.4 edge matrix -------------------------------------------
-    sizes = [1, 2, 3, 4, 5, 15, 16, 17, 18, 31, 32, 33, 59, 60, 61, 63, 64, 65, 255, 256, 257, 511, 512, 1025,
-             2048, 2049, 4095, 4096, 4097, 32767, 32768, 32769, 65535, 65536, 65537, 131072, 131073]
-    kinds = [("T", {"seed": 7}), ("R", {"seed": 3}), ("Z", {}), ("P", {"seed": 2})]
-    for k, extra in kinds:
-        for n in sizes:
+    for k, extra in EDGE_KINDS:
+        for n in EDGE_SIZES:
             spec = {"kind": k, "size": n, **extra}
             entries.append(entry(f"edge_{k}_{n}", spec))
-    for period in [1, 2, 3, 4, 5, 7, 11, 12, 13, 63, 64, 65, 67, 68, 69, 2047, 2048, 2049, 3000]:
+    for period in PERIODS:
         for n in [200, 5000, 65536, 70000]:
             spec = {"kind": "K", "size": n, "seed": 100 + period, "period": period}
             entries.append(entry(f"period_{period}_{n}", spec))
@@ -185,4 +237,4 @@ def main() -> None:
 
 
 if __name__ == "__main__":
-    main()
+    main_bst() if sys.argv[1:] == ["bst"] else main()

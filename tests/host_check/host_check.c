@@ -6,8 +6,9 @@
  * (oracle/snappy_oracle.c, linked in as the checker), never the thing tested.
  *
  *   host_check_asan nodev   no GPU: varint round trips and truncated varints,
- *                           every host entry point's error path (the build
- *                           container; tests/test_host_check.py)
+ *                           every host entry point's error path, the -b
+ *                           compressor's host threads (the build container;
+ *                           tests/test_host_check.py)
  *   host_check_asan gpu     the buffer and FILE* pipelines (ragged sizes, a
  *                           three-chunk input), the sidecar index and a
  *                           corrupted one, malformed streams, pooled host
@@ -27,6 +28,7 @@
 
 size_t oracle_compress(const uint8_t *in, size_t n, uint8_t *out);
 size_t oracle_max_compressed_length(size_t n);
+int oracle_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len);
 int snappy_gen_fill(uint8_t *out, size_t n, int kind, uint64_t seed, int nthreads);
 
 static int g_fail = 0;
@@ -97,10 +99,48 @@ static void check_nodev(void)
     CHECK(snappy_amd_last_status() < 0, "FILE* compress without a device: %d", snappy_amd_last_status());
     rewind(fi);
     CHECK(snappy_decompress(fi, fo) < 0, "FILE* decompress of raw text succeeded");
-    CHECK(snappy_compress_bst(fi, sizeof in, fo) == SNAPPY_AMD_ERR_UNSUPPORTED, "BST stub");
     fclose(fi);
     fclose(fo);
     snappy_amd_host_release();
+}
+
+/* the -b compressor (host threads, no device): every output decodes (oracle)
+ * to its input, the FILE* form writes the buffer form's bytes, a short
+ * output buffer is refused */
+static void check_bst(void)
+{
+    const size_t sizes[] = {1, 4, 15, 16, 17, 100, 65535, 65536, 65537, 200000, (33u << 20) + 777};
+    for (size_t i = 0; i < sizeof sizes / sizeof *sizes; i++) {
+        for (int k = 0; k < 3; k++) {
+            const int kind = "TRP"[k];
+            const size_t n = sizes[i];
+            uint8_t *a = make_input(n, kind, 5 + i);
+            const size_t cap = snappy_max_compressed_length(n);
+            uint8_t *c = malloc(cap), *back = malloc(n);
+            size_t len = 0, dl = 0;
+            CHECK(snappy_compress_bst_buffer(a, n, c, cap, &len) == 0, "bst compress %zu", n);
+            CHECK(oracle_decompress(c, len, back, n, &dl) == 0 && dl == n && !memcmp(back, a, n),
+                  "bst round trip %zu kind %c", n, kind);
+            FILE *fi = tmpfile(), *fo = tmpfile();
+            fwrite(a, 1, n, fi);
+            rewind(fi);
+            CHECK(snappy_compress_bst(fi, n, fo) == 0, "bst FILE* %zu", n);
+            CHECK((size_t)ftell(fo) == len, "bst FILE* length %zu", n);
+            rewind(fo);
+            uint8_t *f = malloc(len ? len : 1);
+            CHECK(fread(f, 1, len, fo) == len && !memcmp(f, c, len), "bst FILE* bytes %zu", n);
+            size_t l2 = 0;
+            CHECK(snappy_compress_bst_buffer(a, n, c, len - 1, &l2) == SNAPPY_AMD_ERR_CAPACITY, "bst short buffer");
+            fclose(fi);
+            fclose(fo);
+            free(a);
+            free(c);
+            free(back);
+            free(f);
+        }
+    }
+    size_t len = 7;
+    CHECK(snappy_compress_bst_buffer(NULL, 0, NULL, 0, &len) == 0 && len == 0, "bst of nothing");
 }
 
 static void round_trip_buffer(size_t n, int kind, uint64_t seed)
@@ -244,6 +284,7 @@ int main(int argc, char **argv)
     check_varints();
     if (!strcmp(mode, "nodev")) {
         check_nodev();
+        check_bst();
     } else {
         const size_t sizes[] = {0, 1, 17, 65535, 65536, 65537, 1000000, (size_t)(150 << 20) + 12345};
         for (size_t i = 0; i < sizeof sizes / sizeof *sizes; i++) round_trip_buffer(sizes[i], 'T', 7 + i);

@@ -85,11 +85,39 @@ def test_no_oracle_in_product():
     pkg = os.path.join(ROOT, "lightweight-snappy_amd")
     for dirpath, _, files in os.walk(pkg):
         for f in files:
-            if f.endswith((".py", ".c", ".hip", ".h", "Makefile")):
+            if f.endswith((".py", ".c", ".cpp", ".cc", ".hip", ".h", ".hpp", "Makefile")):
                 src = open(os.path.join(dirpath, f), errors="ignore").read()
                 assert "liboracle" not in src and "import oracle" not in src, f
     out = subprocess.run(["ldd", snappy_amd.LIB_PATH], capture_output=True, text=True).stdout
     assert "oracle" not in out and "snappy_ref" not in out
+    # nor may the host code open another library or program at run time
+    for f in os.listdir(os.path.join(pkg, "csrc")):
+        src = open(os.path.join(pkg, "csrc", f), errors="ignore").read()
+        for bad in ("dlopen", "execv", "execl", "system(", "popen("):
+            assert bad not in src, (f, bad)
+
+
+def assert_product_config(cfg: str):
+    """A shipped library: both kernel halves built without measurement knobs
+    (the wrong-output ones cannot even compile without SNAPPY_MEASUREMENT_BUILD)."""
+    assert cfg.startswith("compress{") and " decode{" in cfg, cfg
+    for must in ("compress{measurement=0", "decode{measurement=0", "k2_nolit=0", "k4_nofar=0", "k1r_asm=1",
+                 "k4_bpl4=0", "k4_pass_pipe=0"):
+        assert must in cfg, (must, cfg)
+
+
+def test_shipped_library_is_a_product_build():
+    assert_product_config(snappy_amd.build_config())
+
+
+def test_wrong_output_knobs_refuse_to_compile(tmp_path):
+    # -DSNAPPY_K4_NOFAR / -DSNAPPY_K2_NOLIT=1 without SNAPPY_MEASUREMENT_BUILD: #error
+    src = os.path.join(ROOT, "lightweight-snappy_amd", "csrc", "snappy_kernels.hip")
+    for knob in ("-DSNAPPY_K4_NOFAR", "-DSNAPPY_K2_NOLIT=1"):
+        r = subprocess.run(["/opt/rocm/bin/hipcc", "-E", "--offload-arch=gfx950", "-std=c++17", "-I", INC,
+                            "-I", os.path.dirname(src), knob, "--cuda-host-only", src, "-o", str(tmp_path / "x.i")],
+                           capture_output=True, text=True)
+        assert r.returncode != 0 and "measurement builds only" in r.stderr, (knob, r.stderr[-2000:])
 
 
 @pytest.mark.skipif(not os.path.isdir("/root/reference/src"), reason="reference sources only in the build container")

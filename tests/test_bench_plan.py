@@ -88,3 +88,16 @@ def test_plan_matches_library_bounds():
         layout = snappy_amd.STREAMS if unit == 32768 else snappy_amd.SINGLE
         assert sdist.max_output(n, unit) == snappy_amd.Codec.max_output(n, unit, layout)
     assert sdist.pieces_of(20 * GiB + 5, 32768, 8 * GiB) == [8 * GiB, 8 * GiB, 4 * GiB + 5]
+
+
+def test_e2e_piece_larger_than_job_is_the_job():
+    # --e2e-piece-bytes above the job size: the piece (and so the payload slot
+    # and the gather buffer) is the job rounded up to whole units, in both the
+    # sizing bench.py allocates from and the plan it is checked against
+    total = (256 << 20) + 12345
+    a = bench.parse(["--total-bytes", str(total), "--e2e-piece-bytes", str(4 * GiB)])
+    strong, tot, n, e2e, steps, gp = _sizes(a, 1, 0)
+    assert e2e == ((total + 32767) // 32768) * 32768 and steps == 1
+    big = sdist.rank_plan(total, 1, 32768, 8 * GiB, e2e_piece=4 * GiB)
+    same = sdist.rank_plan(total, 1, 32768, 8 * GiB, e2e_piece=e2e)
+    assert big == same

@@ -134,6 +134,19 @@ def test_file_api_header_quirk():
     assert fo2.getvalue() == b""
 
 
+def test_gpu_library_is_a_product_build():
+    """The library these GPU tests load (SNAPPY_AMD_LIB may point elsewhere)
+    reports product knobs for both kernel halves (test_abi.assert_product_config)."""
+    from test_abi import assert_product_config
+    assert_product_config(snappy_amd.build_config())
+
+
+def golden_bst():
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "golden_bst.json")) as f:
+        return json.load(f)
+
+
 def test_cli_round_trip(golden):
     exe = os.path.join(ROOT, "lightweight-snappy_amd", "snappy")
     e = next(x for x in golden["entries"] if x["name"] == "text_1000000")
@@ -145,8 +158,12 @@ def test_cli_round_trip(golden):
         assert sha(open(snp, "rb").read()) == e["out_sha256"]
         subprocess.run([exe, "-d", snp, dec], check=True, capture_output=True)
         assert open(dec, "rb").read() == data
-        r = subprocess.run([exe, "-b", src, snp], capture_output=True)
-        assert r.returncode != 0
+        # -b: the reference's BST-matcher stream (host threads), decoded on the GPU
+        eb = next(x for x in golden_bst()["entries"] if x["name"] == "text_1000000")
+        subprocess.run([exe, "-b", src, snp], check=True, capture_output=True)
+        assert sha(open(snp, "rb").read()) == eb["out_sha256"]
+        subprocess.run([exe, "-d", snp, dec], check=True, capture_output=True)
+        assert open(dec, "rb").read() == data
 
 
 def test_cli_streaming_multi_chunk():
@@ -178,7 +195,8 @@ def test_reference_cli_dropin(golden):
     on the GPU: -c of configs[0]'s 1,000,000-byte text gives the reference's
     golden bytes, -d restores it; the 150 MiB mixed file (three 64 MiB
     pipeline chunks) comes out equal to the one-shot reference stream and
-    round-trips.  src/cmd.c:86-98 calls snappy_compress / snappy_decompress."""
+    round-trips; -b writes the reference's BST-matcher bytes.  src/cmd.c:86-98
+    calls snappy_compress / snappy_compress_bst / snappy_decompress."""
     e = next(x for x in golden["entries"] if x["name"] == "text_1000000")
     one = make_input(e["spec"])
     mixed = np.concatenate([datagen.make("T", 70 << 20, 41), datagen.make("R", 30 << 20, 42),
@@ -199,6 +217,15 @@ def test_reference_cli_dropin(golden):
             assert r.returncode == 0, r.stderr
             assert open(dec, "rb").read() == data, name
             progress(f"dropin {name}: ok")
+        # src/cmd.c:93-94: -b calls snappy_compress_bst; the reference's -b bytes
+        eb = next(x for x in golden_bst()["entries"] if x["name"] == "text_1000000")
+        src, snp, dec = (os.path.join(d, f"bst{x}") for x in ("", ".snp", ".dec"))
+        open(src, "wb").write(one)
+        r = subprocess.run([DROPIN, "-b", src, snp], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        assert sha(open(snp, "rb").read()) == eb["out_sha256"]
+        r = subprocess.run([DROPIN, "-d", snp, dec], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0 and open(dec, "rb").read() == one, r.stderr
 
 
 def test_full_size_streams_1gib(codec):

@@ -33,8 +33,10 @@ def _run(mode, timeout):
 
 
 def test_host_code_sanitized_without_device():
-    if not os.path.exists(BIN):  # the CPU suite may run before build(): make it here
-        subprocess.run(["make", "-C", HERE], check=True, capture_output=True)
+    # (re)made here on every CPU run: a harness that no longer builds fails this
+    # test instead of leaving a stale binary to pass it (build() only warns)
+    r = subprocess.run(["make", "-C", HERE], capture_output=True, text=True)
+    assert r.returncode == 0, "tests/host_check does not build:\n" + (r.stdout + r.stderr)[-4000:]
     env_gpu = os.environ.get("HIP_VISIBLE_DEVICES")
     try:
         os.environ["HIP_VISIBLE_DEVICES"] = "-1"  # no device even on a GPU box

@@ -782,6 +782,11 @@ def main():
         if gloo:
             dist.init_process_group("gloo")
         else:
+            # RCCL's collectives run on the process group's own stream: a high-priority
+            # one takes a hardware queue of its own instead of sharing one of the
+            # process's GPU_MAX_HW_QUEUES (4) with the compute streams, where a C2
+            # collective would wait behind a K1r launch (DESIGN.md 6 lists a rank's streams)
+            os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
@@ -960,7 +965,9 @@ def end_to_end(job: Job, world: int, rank: int, args, cdev, gloo, allgather, tot
     unit, chunk, layout = job.unit, job.chunk, job.layout
     steps_k = job.steps_e2e
     comp_stream = torch.cuda.current_stream(dev)
-    comm = torch.cuda.Stream(dev)
+    # the C2 stream at high priority (a hardware queue of its own, as RCCL's own
+    # stream): the exchange never queues behind the compress of the next step
+    comm = torch.cuda.Stream(dev, priority=-1)
     dstream = torch.cuda.Stream(dev)
     dcodec = snappy_amd.Codec(dev.index)
     dcodec.set_stream(dstream.cuda_stream)

@@ -373,6 +373,19 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
 #ifndef SNAPPY_K1R_ASM_V16
 #define SNAPPY_K1R_ASM_V16 1
 #endif
+// SNAPPY_K1R_ENT16: the entry registers go into the asm loop as they are (u16
+// operands, the tag read as its low byte by SDWA) instead of zero-extended
+// copies, so no v_and and no wait for the refresh's entry reads sits at the
+// loop's entry (the loop waits for them itself)
+#ifndef SNAPPY_K1R_ENT16
+#define SNAPPY_K1R_ENT16 0
+#endif
+// SNAPPY_K1R_ONE_REFRESH: every path that needs a new window sets a flag and the
+// window moves at one place, the top of the round loop (four inlined copies of
+// the refresh left a block of register copies on the way back into the asm loop)
+#ifndef SNAPPY_K1R_ONE_REFRESH
+#define SNAPPY_K1R_ONE_REFRESH 0
+#endif
 template <bool BIG>
 __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
                                          uint32_t hdr_mode, uint64_t header_value,
@@ -444,8 +457,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #define TBL_READ_ENT(adr)                                                                           \
     do {                                                                                           \
         const uint32_t _a = (adr);                                                                 \
-        ent = *(__attribute__((address_space(3))) uint16_t *)(tbl + _a);                           \
-        ent_t = tbl[(_a >> 1) + kTagBase];                                                         \
+        ent = (uint32_t)*(__attribute__((address_space(3))) uint16_t *)(tbl + _a);                 \
+        ent_t = (uint32_t)tbl[(_a >> 1) + kTagBase];                                               \
     } while (0)
 #define TBL_READ(h) TBL_READ3(2 * (h))
 #define TBL_WRITE(s, word) TBL_WRITE3(2 * (s), word)
@@ -637,8 +650,15 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #else
     // the slot's entry and its tag as the loads' own types: a widened copy would
     // make the compiler zero-extend (and wait for) a load where it is issued
+#if SNAPPY_K1R_ENT16 == 2  // (u32 entry registers: the loads' zero extension is the load's own)
+    uint32_t ent = 0, ent_t = 0;
+#elif SNAPPY_K1R_ENT16
+    uint16_t ent = 0;
+    uint16_t ent_t = 0;
+#else
     uint16_t ent = 0;
     uint8_t ent_t = 0;
+#endif
 #endif
     uint32_t adr = 0, word = 0;               // the lane's table record address and its insert word
     uint32_t pdnz = 0;  // the predecessor's tag flag (kV16: its tag)
@@ -878,10 +898,18 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     "v_cndmask_b32_sdwa %[t0], %[pdnz], %[t0], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "             \
     "src0_sel:DWORD src1_sel:WORD_0\n\t"                                                            \
     "v_cmp_eq_u32_e64 %[hm], 0, %[t0]\n\t"
+#if SNAPPY_K1R_ENT16
+#define K1R_ENTT_SEL "src0_sel:DWORD src1_sel:BYTE_0"
+#define K1R_HIT_ENTT                                                                                \
+    "v_cndmask_b32_sdwa %[t0], %[pdnz], %[entt], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "           \
+    "src0_sel:DWORD src1_sel:BYTE_0\n\t" /* and its tag */
+#else
+#define K1R_HIT_ENTT "v_cndmask_b32_e32 %[t0], %[pdnz], %[entt], vcc\n\t" /* and its tag */
+#endif
 #define K1R_HIT_PREDTAG                                                                             \
     "v_cndmask_b32_sdwa %[t1], %[pdc], %[ent], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "             \
     "src0_sel:DWORD src1_sel:WORD_0\n\t" /* the candidate of every lane */                          \
-    "v_cndmask_b32_e32 %[t0], %[pdnz], %[entt], vcc\n\t" /* and its tag */                          \
+    K1R_HIT_ENTT                                                                                    \
     "v_cmp_eq_u32_sdwa %[hm], %[t0], %[word] src0_sel:DWORD src1_sel:WORD_1\n\t"
 #if SNAPPY_K1R_ASM_V16 == 1
 #define K1R_HIT32 K1R_HIT_PREDTAG
@@ -1100,11 +1128,16 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             };
             uint32_t lane0 = p - q0;
             bool went = false;
+#if SNAPPY_K1R_ONE_REFRESH
+            bool rf = !lsw || lane0 + SNAPPY_K1R_RMIN > 62;  // the window moves at the loop top
+            went = rf;  // (there the refresh reads the entries, or reads them after it)
+#else
             if (!lsw || lane0 + SNAPPY_K1R_RMIN > 62) {
                 refresh();
                 lane0 = 1;
                 went = SNAPPY_K1R_WIN_ENT;
             }
+#endif
             // the round's table entries: read right after the round's inserts, so the
             // read is in flight during the verification (each path that writes the table
             // again, and a refresh, reads again); the entry registers have the loads' own
@@ -1114,11 +1147,24 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             // SNAPPY_K1R_LATE_ENT reads at the round's end instead)
             if (!went) TBL_READ_ENT(adr);
             for (;;) {
+#if SNAPPY_K1R_ONE_REFRESH
+                if (rf) {
+                    refresh();
+                    lane0 = 1;
+                    rf = false;
+                    if (!SNAPPY_K1R_WIN_ENT) TBL_READ_ENT(adr);
+                }
+#endif
 #if K1R_ASM_ROUNDS
                 {
                     // the common rounds as one hand-scheduled loop (k1r_asm_rounds below)
                     uint32_t code, fx, cx;
+#if SNAPPY_K1R_ENT16
+#define e32 ent
+#define et32 ent_t
+#else
                     uint32_t e32 = ent, et32 = ent_t;
+#endif
 #ifdef SNAPPY_K1R_RSTAMPS
                     uint64_t ra0, ra1;
                     RSTAMP(ra0);
@@ -1133,13 +1179,22 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     rs_nasm++;
                     rs_code[code < 6 ? code : 0]++;
 #endif
+#if SNAPPY_K1R_ENT16
+#undef e32
+#undef et32
+#else
                     ent = (uint16_t)e32;
                     ent_t = (uint8_t)et32;
+#endif
                     if (code == 1) break;  // skip past the step-1 range, or is_block_end
                     if (code == 2) {       // the window needs to move
+#if SNAPPY_K1R_ONE_REFRESH
+                        rf = true;
+#else
                         refresh();
                         lane0 = 1;
                         if (!SNAPPY_K1R_WIN_ENT) TBL_READ_ENT(adr);
+#endif
                         continue;
                     }
                     if (code >= 4) {  // the round stopped after its inserts: finish it here
@@ -1166,9 +1221,13 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                         if (!(skip <= 64 - SNAPPY_K1R_LSMIN && p <= L - 16)) break;
                         lane0 = p - q0;
                         if (lane0 + SNAPPY_K1R_RMIN > 62) {
+#if SNAPPY_K1R_ONE_REFRESH
+                            rf = true;
+#else
                             refresh();
                             lane0 = 1;
                             if (!SNAPPY_K1R_WIN_ENT) TBL_READ_ENT(adr);
+#endif
                         }
                         continue;
                     }
@@ -1285,10 +1344,14 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 if (__builtin_expect(!(skip <= 64 - SNAPPY_K1R_LSMIN && p <= L - 16), 0)) break;
                 lane0 = p - q0;
                 if (__builtin_expect(lane0 + SNAPPY_K1R_RMIN > 62, 0)) {
+#if SNAPPY_K1R_ONE_REFRESH
+                    rf = true;
+#else
                     refresh();
                     lane0 = 1;
 #ifndef SNAPPY_K1R_LATE_ENT
                     if (!SNAPPY_K1R_WIN_ENT) TBL_READ_ENT(adr);
+#endif
 #endif
                 }
 #ifdef SNAPPY_K1R_LATE_ENT
@@ -2303,6 +2366,10 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
 #ifndef SNAPPY_K4_PASS_V2
 #define SNAPPY_K4_PASS_V2 1
 #endif
+// SNAPPY_K4_PASS_ASM (pass 1): the V2 pass as a software-pipelined asm loop
+#ifndef SNAPPY_K4_PASS_ASM
+#define SNAPPY_K4_PASS_ASM 0
+#endif
 // SNAPPY_K4_PASS_PIPE (with V2): passes software-pipelined by one stage
 #ifndef SNAPPY_K4_PASS_PIPE
 #define SNAPPY_K4_PASS_PIPE 0
@@ -2750,7 +2817,143 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             }
 #else
             uint32_t cb = 0;  // elements starting before the pass
-#if SNAPPY_K4_PASS_V2 && SNAPPY_K4_PASS_PIPE
+#if SNAPPY_K4_PASS_ASM
+            if constexpr (!BACK) {
+            // the V2 pass (below) as one hand-scheduled asm loop, software-pipelined by
+            // one stage: the element lookup of pass i + 1 (bitmap read-back, mbcnt, the
+            // two ds_bpermute) is issued before pass i waits for its window / ring bytes,
+            // and its far load (a copy source older than the ring, from HBM) and window
+            // read before pass i + 1 begins, so each wait covers one pass's latency
+            // instead of the compiler's lgkmcnt(0) / vmcnt(0) after every load
+            // (DESIGN.md 4.3).  Every wait is written out: LDS operations complete in
+            // issue order (lgkmcnt(N) = all but the N youngest), the far load is the
+            // only vector-memory operation in flight.  Wait states: a VALU-written mask
+            // is read by VALU >= 2 instructions later, v_rcp's result 1 later.  exec is
+            // saved and restored around every masked region.  vcc carries the pass's
+            // 64 bitmap bits (lo / hi halves are nameable).  Output bytes, ring and
+            // window addresses are those of the V2 loop; the LDS array starts at
+            // address 0 (checked below), so window bytes are at 0 + t and the ring at
+            // kK4RingAt + (x & M).
+            const uint32_t kx = e_t == 0 ? 256 * ws + e_lsrc - e_op : 0u - e_info;
+            if (__builtin_expect((uint32_t)(uintptr_t)wb != 0, 0)) __builtin_trap();
+            uint32_t sP, si2, scb, sA, sB, sF;
+            uint64_t mp, ml, mf, mc, mo, sv;
+            uint32_t vo, vt, vfo, vfx, vfv, vlb, vrv, vva, vtm, vtn;
+#define K4A1                                                                                         \
+    "s_add_u32 %[sA], %[i2], 1\n\t"                                                                \
+    "v_readlane_b32 vcc_lo, %[bm], %[i2]\n\t" /* (an SALU-written lane select: one apart) */        \
+    "v_readlane_b32 vcc_hi, %[bm], %[sA]\n\t"                                                      \
+    "s_and_b32 %[sA], vcc_lo, 1\n\t"                                                               \
+    "s_add_u32 %[sA], %[sA], %[cb]\n\t"                                                            \
+    "s_sub_u32 %[sA], %[sA], 1\n\t" /* cb - 1 + (sm & 1) */                                        \
+    "s_bcnt1_i32_b64 %[sB], vcc\n\t"                                                               \
+    "s_add_u32 %[cb], %[cb], %[sB]\n\t"                                                            \
+    "s_lshr_b64 vcc, vcc, 1\n\t"                                                                   \
+    "v_mov_b32 %[vtm], %[sA]\n\t"                                                                  \
+    "v_mbcnt_lo_u32_b32 %[vtm], vcc_lo, %[vtm]\n\t"                                                \
+    "v_mbcnt_hi_u32_b32 %[vtm], vcc_hi, %[vtm]\n\t" /* the byte's element */                       \
+    "v_lshlrev_b32 %[vtm], 2, %[vtm]\n\t"                                                          \
+    "ds_bpermute_b32 %[vfo], %[vtm], %[kop]\n\t"                                                   \
+    "ds_bpermute_b32 %[vfx], %[vtm], %[kx]\n\t"                                                    \
+    "s_add_u32 %[i2], %[i2], 2\n\t"
+#define K4A2                                                                                         \
+    "v_cmp_gt_u32_e64 %[mp], %[opend], %[vo]\n\t" /* pend */                                       \
+    "v_cmp_gt_i32_e64 %[ml], 0, %[vfo]\n\t"       /* literal */                                    \
+    "v_add_u32_e32 %[vt], %[vo], %[vfx]\n\t"      /* window address or copy source */              \
+    "v_cmp_gt_u32_e64 %[mf], %[lo], %[vt]\n\t"                                                     \
+    "s_andn2_b64 %[mf], %[mf], %[ml]\n\t"                                                          \
+    "s_and_b64 %[mf], %[mf], %[mp]\n\t"           /* far: older than the ring */                   \
+    "s_and_saveexec_b64 %[sv], %[mf]\n\t"                                                          \
+    "global_load_ubyte %[vfv], %[vt], %[dst]\n\t"                                                  \
+    "s_mov_b64 exec, %[sv]\n\t"                                                                    \
+    "v_add_u32_e32 %[vtn], 0xfffffd00, %[vt]\n\t"                                                  \
+    "v_min3_u32 %[vtn], %[vt], %[vtn], %[wmax]\n\t"                                                \
+    "ds_read_u8 %[vlb], %[vtn]\n\t"               /* the window byte */
+            if (op < op_end) {
+                asm volatile(
+                    "s_mov_b32 %[P], %[op]\n\t"
+                    "s_mov_b32 %[i2], 0\n\t"
+                    "s_mov_b32 %[cb], 0\n\t"
+                    "v_add_u32_e32 %[vo], %[op], %[lane]\n\t"
+                    K4A1
+                    "s_waitcnt lgkmcnt(0)\n\t"
+                    K4A2
+                    "L%=_top:\n\t"
+                    // ---- pass P, stage B: an overlapping copy's source (byte d mod off)
+                    "s_or_b64 %[mc], %[ml], %[mf]\n\t"
+                    "s_andn2_b64 %[mc], %[mp], %[mc]\n\t"      /* copy from the ring */
+                    "v_cmp_ge_u32_e64 %[mo], %[vt], %[vfo]\n\t"
+                    "s_and_b64 %[mo], %[mo], %[mc]\n\t"
+                    "s_cbranch_scc0 L%=_noov\n\t"
+                    "s_and_saveexec_b64 %[sv], %[mo]\n\t"
+                    "v_sub_u32_e32 %[vtn], 0, %[vfx]\n\t"      /* off */
+                    "v_cvt_f32_u32_e32 %[vtn], %[vtn]\n\t"
+                    "v_sub_u32_e32 %[vtm], %[vo], %[vfo]\n\t"  /* d */
+                    "v_cvt_f32_u32_e32 %[vtm], %[vtm]\n\t"
+                    "v_rcp_f32_e32 %[vtn], %[vtn]\n\t"
+                    "s_nop 0\n\t"
+                    "v_fmaak_f32 %[vtm], %[vtn], %[vtm], 0x38d1b717\n\t"  /* d / off + 1e-4 */
+                    "v_cvt_u32_f32_e32 %[vtm], %[vtm]\n\t"
+                    "v_mad_i32_i24 %[vt], %[vtm], %[vfx], %[vt]\n\t"       /* t - qd * off */
+                    "s_mov_b64 exec, %[sv]\n"
+                    "L%=_noov:\n\t"
+                    "v_and_b32_e32 %[vtm], 0xfff, %[vt]\n\t"
+                    "ds_read_u8 %[vrv], %[vtm] offset:%[ringat]\n\t"     /* the ring byte */
+                    "v_cmp_ge_u32_e64 %[mo], %[vt], %[P]\n\t"
+                    "s_and_b64 %[mo], %[mo], %[mc]\n\t"        /* a source inside this pass */
+                    "s_cselect_b32 %[sF], 1, 0\n\t"
+                    // ---- pass P + 64, stage A (element lookup)
+                    K4A1
+                    "s_waitcnt lgkmcnt(2)\n\t"                 /* window and ring bytes of pass P */
+                    "s_waitcnt vmcnt(0)\n\t"                   /* its far bytes */
+                    "v_cndmask_b32_e64 %[vva], %[vrv], %[vlb], %[ml]\n\t"
+                    "v_cndmask_b32_e64 %[vva], %[vva], %[vfv], %[mf]\n\t"
+                    "s_cmp_lg_u32 %[sF], 0\n\t"
+                    "s_cbranch_scc1 L%=_inpass\n"
+                    "L%=_write:\n\t"
+                    "v_and_b32_e32 %[vtm], 0xfff, %[vo]\n\t"
+                    "s_and_saveexec_b64 %[sv], %[mp]\n\t"
+                    "ds_write_b8 %[vtm], %[vva] offset:%[ringat]\n\t"
+                    "s_mov_b64 exec, %[sv]\n\t"
+                    "s_add_u32 %[P], %[P], 64\n\t"
+                    "s_cmp_ge_u32 %[P], %[opend]\n\t"
+                    "s_cbranch_scc1 L%=_exit\n\t"
+                    // ---- pass P + 64, stage A (its bytes' sources)
+                    "v_add_u32_e32 %[vo], 64, %[vo]\n\t"
+                    "s_waitcnt lgkmcnt(1)\n\t"                 /* its two bpermutes (the write may pend) */
+                    K4A2
+                    "s_branch L%=_top\n"
+                    // ---- rare: sources inside the pass, by pointer jumping over lanes
+                    "L%=_inpass:\n\t"
+                    "v_subrev_u32_e32 %[vtm], %[P], %[vt]\n\t"
+                    "v_cndmask_b32_e64 %[vtm], %[lane], %[vtm], %[mo]\n"
+                    "L%=_pj:\n\t"
+                    "v_lshlrev_b32_e32 %[vtn], 2, %[vtm]\n\t"
+                    "ds_bpermute_b32 %[vfv], %[vtn], %[vtm]\n\t"
+                    "s_waitcnt lgkmcnt(0)\n\t"
+                    "v_cmp_ne_u32_e64 %[mo], %[vfv], %[vtm]\n\t"
+                    "v_mov_b32_e32 %[vtm], %[vfv]\n\t"
+                    "s_cmp_lg_u64 %[mo], 0\n\t"
+                    "s_cbranch_scc1 L%=_pj\n\t"
+                    "v_lshlrev_b32_e32 %[vtn], 2, %[vtm]\n\t"
+                    "ds_bpermute_b32 %[vva], %[vtn], %[vva]\n\t"
+                    "s_waitcnt lgkmcnt(0)\n\t"
+                    "s_branch L%=_write\n"
+                    "L%=_exit:\n\t"
+                    "s_waitcnt lgkmcnt(0)"
+                    : [P] "=&s"(sP), [i2] "=&s"(si2), [cb] "=&s"(scb), [sA] "=&s"(sA), [sB] "=&s"(sB),
+                      [sF] "=&s"(sF), [mp] "=&s"(mp), [ml] "=&s"(ml), [mf] "=&s"(mf), [mc] "=&s"(mc),
+                      [mo] "=&s"(mo), [sv] "=&s"(sv), [vo] "=&v"(vo), [vt] "=&v"(vt), [vfo] "=&v"(vfo),
+                      [vfx] "=&v"(vfx), [vfv] "=&v"(vfv), [vlb] "=&v"(vlb), [vrv] "=&v"(vrv), [vva] "=&v"(vva),
+                      [vtm] "=&v"(vtm), [vtn] "=&v"(vtn)
+                    : [bm] "v"(bm), [kop] "v"(kop), [kx] "v"(kx), [lane] "v"(lane), [op] "s"(op),
+                      [opend] "s"(op_end), [lo] "s"(lo), [dst] "s"(dst), [wmax] "s"(783u), [ringat] "i"(kK4RingAt)
+                    : "vcc", "scc", "memory");
+            }
+#undef K4A1
+#undef K4A2
+            } else
+#elif SNAPPY_K4_PASS_V2 && SNAPPY_K4_PASS_PIPE
             if constexpr (!BACK) {
             const uint32_t kx = e_t == 0 ? 256 * ws + e_lsrc - e_op : 0u - e_info;
             // software-pipelined passes: stage A of pass i + 1 (element lookup, address,

@@ -39,7 +39,10 @@ if [ -f $D/snappy_pipeline.cpp ]; then
         -c $D/snappy_pipeline.cpp -o $P/build/pipe_$NAME.o
     PIPE=$P/build/pipe_$NAME.o
 fi
+# the working tree's -b compressor and weak stubs of newer entry points (tools/variant_stub.c)
+gcc -O2 -fPIC -std=gnu11 -pthread -Iinclude -c $P/csrc/bst_host.c -o $P/build/bst_var.o
+gcc -O2 -fPIC -std=gnu11 -Iinclude -c tools/variant_stub.c -o $P/build/stub_var.o
 hipcc --offload-arch=${VARCH:-gfx950} -shared -fPIC -o $P/variants/libsnappy_amd_$NAME.so $P/build/kc_$NAME.o $P/build/kd_$NAME.o \
-    $P/build/dev_$NAME.o $PIPE $P/build/host_var.o
+    $P/build/dev_$NAME.o $PIPE $P/build/host_var.o $P/build/bst_var.o $P/build/stub_var.o
 rm -rf $D
 echo "built $NAME ($REV $*)"

@@ -362,30 +362,13 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
     return x - v;
 }
 
-// SNAPPY_K1R_ASM_V16: the lane data carry the in-window predecessor's tag
-// (pdnz), so the hit test selects the candidate's tag and compares it once
-// with the lane's (16-bit field: a lane past the window has bit 24 of its word
-// set and never matches) -- two VALU instead of three.  1 = both kernels, 2 =
-// K1r64 only (A/B, profiles/r05za_*: 64 KiB blocks 15.04-15.08 -> 14.51 ms per
-// GiB; 32 KiB streams 12.89 -> 13.04 there, but with the loop's placement pinned
-// at its best offset for each build 12.56 -> 12.34-12.36, profiles/r05zs_*: the
-// first K1r figure was a placement effect)
-#ifndef SNAPPY_K1R_ASM_V16
-#define SNAPPY_K1R_ASM_V16 1
-#endif
-// SNAPPY_K1R_ENT16: the entry registers go into the asm loop as they are (u16
-// operands, the tag read as its low byte by SDWA) instead of zero-extended
-// copies, so no v_and and no wait for the refresh's entry reads sits at the
-// loop's entry (the loop waits for them itself)
-#ifndef SNAPPY_K1R_ENT16
-#define SNAPPY_K1R_ENT16 0
-#endif
-// SNAPPY_K1R_ONE_REFRESH: every path that needs a new window sets a flag and the
-// window moves at one place, the top of the round loop (four inlined copies of
-// the refresh left a block of register copies on the way back into the asm loop)
-#ifndef SNAPPY_K1R_ONE_REFRESH
-#define SNAPPY_K1R_ONE_REFRESH 0
-#endif
+// The lane data carry the in-window predecessor's tag (pdnz), so the hit test
+// selects the candidate's tag and compares it once with the lane's (16-bit
+// field: a lane past the window has bit 24 of its word set and never matches)
+// -- two VALU instead of three (V16: 64 KiB blocks 15.04-15.08 -> 14.51 ms per
+// GiB, 32 KiB streams at matched loop placement 12.56 -> 12.34-12.36;
+// profiles/r05za_*, r05zs_*)
+
 template <bool BIG>
 __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_t n, uint32_t unit,
                                          uint32_t hdr_mode, uint64_t header_value,
@@ -402,22 +385,6 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     // the next record's), a ds_write_b16 + ds_write_b8_d16_hi store one; the
     // highest lane wins a record shared within one instruction pair
     // (tools/micro/lds_packed3.hip).  12 units/CU (with the VGPR limit).
-#ifdef SNAPPY_K1R_PACKED3
-    __shared__ __attribute__((aligned(16))) uint8_t tbl_[3 * kTable + 8];
-    constexpr uint32_t kDummy = 3 * kTable + 4;  // a record nobody reads: the target of non-inserting lanes
-    auto *const tbl = (__attribute__((address_space(3))) uint8_t *)tbl_;
-#define TBL_READ3(adr) (*(__attribute__((address_space(3))) u32u *)(tbl + (adr)))
-#define TBL_WRITE3(adr, word)                                                                       \
-    do {                                                                                           \
-        const uint32_t _a = (adr), _w = (word);                                                    \
-        *(__attribute__((address_space(3))) u16u *)(tbl + _a) = (uint16_t)_w;                       \
-        tbl[_a + 2] = (uint8_t)(_w >> 16);                                                         \
-    } while (0)
-#define TBL_ADR(h) (3 * (h))
-#define TBL_READ_ENT(adr) do { ent = TBL_READ3(adr); ent_t = ent >> 16; } while (0)
-#define TBL_READ(h) TBL_READ3(3 * (h))
-#define TBL_WRITE(s, word) TBL_WRITE3(3 * (s), word)
-#else
     // The same 12 KiB as two aligned arrays: u16 positions at byte 2 * slot and
     // u8 tags at kTagBase + slot, so no table access is unaligned (the packed
     // 3-byte records measured SQ_LDS_UNALIGNED_STALL 8.5e9 per 1 GiB launch:
@@ -457,24 +424,16 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #define TBL_READ_ENT(adr)                                                                           \
     do {                                                                                           \
         const uint32_t _a = (adr);                                                                 \
-        ent = (uint32_t)*(__attribute__((address_space(3))) uint16_t *)(tbl + _a);                 \
-        ent_t = (uint32_t)tbl[(_a >> 1) + kTagBase];                                               \
+        ent = *(__attribute__((address_space(3))) uint16_t *)(tbl + _a);                           \
+        ent_t = tbl[(_a >> 1) + kTagBase];                                                         \
     } while (0)
 #define TBL_READ(h) TBL_READ3(2 * (h))
 #define TBL_WRITE(s, word) TBL_WRITE3(2 * (s), word)
-#endif
-// SNAPPY_K1R_TAG1: the tag as the 8 product bits below the table index, ((v *
+// The tag: the 8 product bits below the table index, ((v *
 // kMul) >> (shift - 8)) & 0xFF, instead of a second multiply (any function of
 // the 4 bytes filters candidates: equal bytes give equal tags, and a tag
 // collision is verified like any hit)
-#ifndef SNAPPY_K1R_TAG1
-#define SNAPPY_K1R_TAG1 1
-#endif
-#if SNAPPY_K1R_TAG1
 #define TAG_OF(v) __builtin_amdgcn_ubfe((v) * kMul, shift - 8, 8)
-#else
-#define TAG_OF(v) (((v) * kTagMul) >> 24)
-#endif
 // an insert group: the lanes where cond holds write their record; the others
 // write the dummy record (one instruction stream, no exec change: masking
 // them off measured 3 % slower, profiles/r03j_ab_k1r_masked_*)
@@ -645,24 +604,12 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     // rotated: dword q0/4 + i sits at lane (dr + i) % 64 (ds_bpermute wraps addr[7:2])
     uint32_t q0 = 0, d0 = 0, dr = 0, dv = 0, bv = 0, hv = 0;
     uint32_t pdl1 = 0, pdc = 0;               // lane-space data: predecessor lane + 1, its position
-#ifdef SNAPPY_K1R_PACKED3
-    uint32_t ent = 0, ent_t = 0;              // the slot's entry and its tag
-#else
     // the slot's entry and its tag as the loads' own types: a widened copy would
     // make the compiler zero-extend (and wait for) a load where it is issued
-#if SNAPPY_K1R_ENT16 == 2  // (u32 entry registers: the loads' zero extension is the load's own)
-    uint32_t ent = 0, ent_t = 0;
-#elif SNAPPY_K1R_ENT16
-    uint16_t ent = 0;
-    uint16_t ent_t = 0;
-#else
     uint16_t ent = 0;
     uint8_t ent_t = 0;
-#endif
-#endif
     uint32_t adr = 0, word = 0;               // the lane's table record address and its insert word
-    uint32_t pdnz = 0;  // the predecessor's tag flag (kV16: its tag)
-    constexpr bool kV16 = SNAPPY_K1R_ASM_V16 == 1 || (SNAPPY_K1R_ASM_V16 == 2 && BIG);
+    uint32_t pdnz = 0;  // the predecessor's tag
     uint64_t m_win = 0, m_win17 = 0;
     bool lsw = false;  // the lane-space data describe the current window
 // SNAPPY_K1R_WIN_ALIGN: a window's per-lane BE32 by v_alignbit from (p - 1) / 4
@@ -698,11 +645,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             const uint32_t _b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((_k + 1) << 2), (int)dv); \
             bv = funnel_bytes(_a, _b, perm_sel((q0 + lane) & 3));                                 \
         }                                                                                          \
-        if (SNAPPY_K1R_TAG1) {                                                                     \
+        {                                                                                          \
             const uint32_t _pr = bv * kMul;                                                        \
             hv = (_pr >> shift) | (__builtin_amdgcn_ubfe(_pr, shift - 8, 8) << 16);                \
-        } else {                                                                                   \
-            hv = ((bv * kMul) >> shift) | (TAG_OF(bv) << 16);                                      \
         }                                                                                          \
     } while (0)
 // SNAPPY_K1R_WIN_ENT: a window refresh reads the new window's table entries as
@@ -722,18 +667,15 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
         pdl1 = _bits ? lane - _pd + 1 - (_pd == 1 ? 1u : 0u) : 0xFFFFFF00u; /* signed: below every lane0 */ \
         pdc = q0 + lane - _pd;                                                                     \
         const uint32_t _hp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - _pd) << 2), (int)hv); \
-        /* 0 iff the predecessor's tag matches; V16: the predecessor's tag */                       \
-        pdnz = kV16 ? (_hp >> 16) & 0xFFu : (_hp == hv ? 0u : 1u);                                 \
+        /* the predecessor's tag */                                                                \
+        pdnz = (_hp >> 16) & 0xFFu;                                                                \
         /* probe lanes: <= 62 and not past is_block_end (L - p >= 16, 17 at skip 64) */           \
         const int32_t _w16 = (int32_t)(L - 16 - q0), _w17 = (int32_t)(L - 17 - q0);              \
         const bool _inw = (int32_t)lane <= _w16 && lane <= 62;                                     \
         m_win = __ballot(_inw);                                                                    \
         m_win17 = __ballot((int32_t)lane <= _w17 && lane <= 62);                                   \
         word = (q0 + lane) | (hv & 0xFF0000u);                                                     \
-        if (!_inw) { /* the asm hit test sees the window mask in the lane data */                  \
-            word |= 1u << 24;                                                                      \
-            if (!kV16) pdnz = 1;                                                                   \
-        }                                                                                          \
+        if (!_inw) word |= 1u << 24; /* the asm hit test sees the window mask in the lane data */   \
         lsw = true; /* the caller reads ent */                                                     \
     } while (0)
 
@@ -829,8 +771,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     // (60 % of text matches are there) 17.49-17.52 (its extra LDS traffic and
     // issue cost more than the latency it hides).  SNAPPY_K1R_CXX_ROUNDS keeps
     // the C++ round (the statistics and stamp builds always do).
-#if !defined(SNAPPY_K1R_STATS) && !defined(SNAPPY_K1R_LSTAMPS) && !defined(SNAPPY_K1R_CXX_ROUNDS) && \
-    !defined(SNAPPY_K1R_PACKED3)
+#if !defined(SNAPPY_K1R_STATS) && !defined(SNAPPY_K1R_LSTAMPS) && !defined(SNAPPY_K1R_CXX_ROUNDS)
 #define K1R_ASM_ROUNDS 1
 #else
 #define K1R_ASM_ROUNDS 0
@@ -851,7 +792,10 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 //    s_set_gpr_idx on SRC0 and SRC1 (lanes >= l0 take R; V15); K1r64 reads ring
 //    registers (c / 256) mod 128: a candidate whose segment left the ring is
 //    gathered from the input (global_load_dword, byte-swapped to the ring's
-//    big-endian dwords; V19), the wrap pair 127 / 0 leaves for the C++ round
+//    big-endian dwords; V19), the wrap pair 127 / 0 by a select of v129 / v2
+//    without a register index (round 6; it left for the C++ round before:
+//    64 KiB blocks 14.11 -> 14.14-14.18 ms per GiB unpinned, within the loop
+//    placement's +-2 %, profiles/r06e_ab_*)
 //  * the previous round's token drained into tka / tkb during the gathers, its
 //    first word by one s_pack_ll_b32_b16 (V9); lo0 = lane0 - (lane0 < f) by
 //    s_subb (V5)
@@ -862,8 +806,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 //  * the prefix length per lane as (clz(xor) >> 3) | 4 lane, read back from the
 //    first differing dword (V3, V7); skip is not reset by a hit round (a pending
 //    token implies skip 32, V8); the clamp to the block end only on the exit path
-// The loop runs in uniform control flow with all 64 lanes live, so it restores
-// exec to all ones after each masked insert (exec cannot be declared clobbered).
+// Each masked insert restores exec to its value where the statement runs (sx,
+// read by the compiler: the statement runs in uniform control flow with all
+// 64 lanes live, and exec cannot be declared clobbered).
 // SNAPPY_K1R_PAD32 / SNAPPY_K1R_PAD64: the loop's first instruction placed
 // at byte 4*PAD of a 64-byte line (-1: wherever the code before it ends).  The
 // same loop code placed 4 bytes apart measured 1.8 % apart (profiles/r05zn_*,
@@ -888,45 +833,30 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     "s_cbranch_scc1 L%=_far\n\t"                                                                   \
     "s_bfe_u32 %[s0], %[c], 0x70008\n\t"                                                           \
     "s_cmp_eq_u32 %[s0], 127\n\t"                                                                  \
-    "s_cbranch_scc1 L%=_x3\n\t"
+    "s_cbranch_scc1 L%=_wrap\n\t" /* the wrap pair 127 / 0: gathered below, no register index */
 #define K1R_SEGHI64(seg_hi) "s"(((seg_hi) - kRegs) << 8)
-#define K1R_HIT_TAGDIFF                                                                             \
-    "v_xor_b32_sdwa %[t0], %[entt], %[word] dst_sel:DWORD dst_unused:UNUSED_PAD "                    \
-    "src0_sel:DWORD src1_sel:WORD_1\n\t"                                                            \
-    "v_cndmask_b32_sdwa %[t1], %[pdc], %[ent], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "             \
-    "src0_sel:DWORD src1_sel:WORD_0\n\t" /* the candidate of every lane */                          \
-    "v_cndmask_b32_sdwa %[t0], %[pdnz], %[t0], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "             \
-    "src0_sel:DWORD src1_sel:WORD_0\n\t"                                                            \
-    "v_cmp_eq_u32_e64 %[hm], 0, %[t0]\n\t"
-#if SNAPPY_K1R_ENT16
-#define K1R_ENTT_SEL "src0_sel:DWORD src1_sel:BYTE_0"
-#define K1R_HIT_ENTT                                                                                \
-    "v_cndmask_b32_sdwa %[t0], %[pdnz], %[entt], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "           \
-    "src0_sel:DWORD src1_sel:BYTE_0\n\t" /* and its tag */
-#else
-#define K1R_HIT_ENTT "v_cndmask_b32_e32 %[t0], %[pdnz], %[entt], vcc\n\t" /* and its tag */
-#endif
 #define K1R_HIT_PREDTAG                                                                             \
     "v_cndmask_b32_sdwa %[t1], %[pdc], %[ent], vcc dst_sel:DWORD dst_unused:UNUSED_PAD "             \
     "src0_sel:DWORD src1_sel:WORD_0\n\t" /* the candidate of every lane */                          \
-    K1R_HIT_ENTT                                                                                    \
+    "v_cndmask_b32_e32 %[t0], %[pdnz], %[entt], vcc\n\t" /* and its tag */                          \
     "v_cmp_eq_u32_sdwa %[hm], %[t0], %[word] src0_sel:DWORD src1_sel:WORD_1\n\t"
-#if SNAPPY_K1R_ASM_V16 == 1
 #define K1R_HIT32 K1R_HIT_PREDTAG
-#else
-#define K1R_HIT32 K1R_HIT_TAGDIFF
-#endif
-#if SNAPPY_K1R_ASM_V16 >= 1
 #define K1R_HIT64 K1R_HIT_PREDTAG
-#else
-#define K1R_HIT64 K1R_HIT_TAGDIFF
-#endif
 #define K1R_DRAIN                                                                                   \
     "s_mov_b32 m0, %[pend]\n\t" /* (gfx950 refuses two SGPRs in a v_writelane: m0 stays) */          \
     "v_writelane_b32 %[tka], %[dka], m0\n\t"                                                        \
     "v_writelane_b32 %[tkb], %[dkb], m0\n\t"                                                        \
     "s_add_u32 %[pend], %[pend], %[dkn]\n\t"
 #define K1R_SKIPFIX "s_cmp_eq_u32 %[dkn], 0\n\ts_cselect_b32 %[skip], %[skip], 32\n\t"
+// the round's inserts (lanes lo0 .. f, or the misses' lanes) under an exec mask,
+// exec restored to its value at the statement (sx), then the next round's entries
+#define K1R_INSERTS(cnt, lo)                                                                        \
+    "s_bfm_b64 exec, " cnt ", " lo "\n\t"                                                          \
+    "ds_write_b16 %[adr], %[word]\n\t"                                                              \
+    "ds_write_b8_d16_hi %[adrt], %[word] offset:%[tagb]\n\t"                                        \
+    "s_mov_b64 exec, %[sx]\n\t"                                                                     \
+    "ds_read_u16 %[ent], %[adr]\n\t" /* the next round's entries */                                  \
+    "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"
 #define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, CAND, SEGHI, HIT, PAD)                         \
     do {                                                                                            \
         uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4;                            \
@@ -971,12 +901,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "v_mov_b32_dpp %[t4], %[t3] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
             "v_alignbit_b32 %[t2], %[t2], %[t1], %[t0]\n\t"                                         \
             "v_perm_b32 %[t3], %[t3], %[t4], %[s3]\n\t"                                             \
-            "s_bfm_b64 exec, %[s2], %[s0]\n\t"                                                      \
-            "ds_write_b16 %[adr], %[word]\n\t"                                                      \
-            "ds_write_b8_d16_hi %[adrt], %[word] offset:%[tagb]\n\t"                                \
-            "s_mov_b64 exec, -1\n\t"                                                                \
-            "ds_read_u16 %[ent], %[adr]\n\t" /* the next round's entries */                          \
-            "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"                                        \
+            K1R_INSERTS("%[s2]", "%[s0]")                                                           \
             "v_cmp_ne_u32_e32 vcc, %[t2], %[t3]\n\t"                                                \
             "v_xor_b32_e32 %[t2], %[t2], %[t3]\n\t"                                                 \
             "v_ffbh_u32_e32 %[t2], %[t2]\n\t"                                                       \
@@ -1013,12 +938,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "s_add_u32 %[s2], %[skip], %[s0]\n\t"                                                   \
             "s_add_i32 %[s3], %[s2], -1\n\t"                                                        \
             "s_add_u32 %[c], %[s0], 1\n\t" /* (c is free on this path) */                          \
-            "s_bfm_b64 exec, %[c], %[s1]\n\t" /* lanes lane0 - 1 .. lane0 - 1 + nk */              \
-            "ds_write_b16 %[adr], %[word]\n\t"                                                      \
-            "ds_write_b8_d16_hi %[adrt], %[word] offset:%[tagb]\n\t"                                \
-            "s_mov_b64 exec, -1\n\t"                                                                \
-            "ds_read_u16 %[ent], %[adr]\n\t"                                                        \
-            "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"                                        \
+            K1R_INSERTS("%[c]", "%[s1]") /* lanes lane0 - 1 .. lane0 - 1 + nk */                    \
             "s_lshr_b32 %[s3], %[s3], 5\n\t" /* the last probe steps by 2 at skip 64 */             \
             "s_add_u32 %[lane0], %[s1], %[s0]\n\t" /* lane0 - 1 + nk + the step-2 probe */          \
             "s_add_u32 %[lane0], %[lane0], %[s3]\n\t"                                               \
@@ -1044,6 +964,14 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "s_waitcnt vmcnt(0)\n\t"                                                                \
             "v_perm_b32 %[t3], %[t3], %[t3], %[s1]\n\t" /* big-endian, as the ring registers */    \
             "s_branch L%=_farret\n"                                                                 \
+            "L%=_wrap:\n\t" /* K1r64: registers 127 (v129, lanes >= l0) and 0 (v2) */               \
+            "s_bfe_u32 %[s1], %[c], 0x60002\n\t"                                                    \
+            "v_cmp_le_u32_e32 vcc, %[s1], %[lane]\n\t"                                              \
+            "v_add_u32_e32 %[t1], %[c], %[lane4]\n\t"                                               \
+            "s_nop 0\n\t"                                                                            \
+            "v_cndmask_b32_e32 %[t3], v2, v129, vcc\n\t"                                            \
+            "ds_bpermute_b32 %[t3], %[t1], %[t3]\n\t"                                               \
+            "s_branch L%=_farret\n"                                                                 \
             "L%=_x5:\n\ts_mov_b32 %[code], 5\n"                                                     \
             "L%=_end:\n\t"                                                                          \
             K1R_SKIPFIX                                                                             \
@@ -1060,6 +988,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
               [dv] "v"(dv),                                                                         \
               [pdl1] "v"(pdl1), [pdc] "v"(pdc), [pdnz] "v"(pdnz), [adr] "v"(adr), [adrt] "v"(adr >> 1), \
               [word] "v"(word), [lane] "v"(lane), [lane4] "v"(lane << 2), [srcb] "s"(src),            \
+              [sx] "s"(__builtin_amdgcn_read_exec()), /* exec here (the compiler reads it once) */     \
               [skipmax] "i"(64 - DMAX), [dmask] "i"((1u << DMAX) - 1), [lsmax] "i"(64 - SNAPPY_K1R_LSMIN), \
               [l0max] "i"(62 - SNAPPY_K1R_RMIN), [tagb] "i"(kTagBase), "{v[2:33]}"(g0), "{v[34:65]}"(g1), \
               "{v[66:97]}"(g2), "{v[98:129]}"(g3)                                                      \
@@ -1112,13 +1041,11 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 // BIG: the window move waits vmcnt(0) for its staged LDS-DMA, and vmcnt
                 // counts stores too (in issue order): flush after the move, so that
                 // wait never covers this refresh's token stores
-#ifndef SNAPPY_K1R_FLUSH_FIRST
                 if constexpr (BIG) {
                     const bool fl = pend + dkn > 48;
                     WINDOW_LS(p - 1);
                     if (fl) flush_tokens();
                 } else
-#endif
                 {
                     if (pend + dkn > 48) flush_tokens();
                     WINDOW_LS(p - 1);
@@ -1128,43 +1055,25 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             };
             uint32_t lane0 = p - q0;
             bool went = false;
-#if SNAPPY_K1R_ONE_REFRESH
-            bool rf = !lsw || lane0 + SNAPPY_K1R_RMIN > 62;  // the window moves at the loop top
-            went = rf;  // (there the refresh reads the entries, or reads them after it)
-#else
             if (!lsw || lane0 + SNAPPY_K1R_RMIN > 62) {
                 refresh();
                 lane0 = 1;
                 went = SNAPPY_K1R_WIN_ENT;
             }
-#endif
             // the round's table entries: read right after the round's inserts, so the
             // read is in flight during the verification (each path that writes the table
             // again, and a refresh, reads again); the entry registers have the loads' own
             // u16 / u8 types, or the compiler zero-extends -- and waits for -- each load
             // where it is issued (round 3: that wait made this order 8 % slower; now
-            // text32k 16.19 -> 16.18 ms, 64 KiB blocks 19.37 -> 19.20, profiles/r03s2b_*;
-            // SNAPPY_K1R_LATE_ENT reads at the round's end instead)
+            // text32k 16.19 -> 16.18 ms, 64 KiB blocks 19.37 -> 19.20, profiles/r03s2b_*,
+            // against reading at the round's end)
             if (!went) TBL_READ_ENT(adr);
             for (;;) {
-#if SNAPPY_K1R_ONE_REFRESH
-                if (rf) {
-                    refresh();
-                    lane0 = 1;
-                    rf = false;
-                    if (!SNAPPY_K1R_WIN_ENT) TBL_READ_ENT(adr);
-                }
-#endif
 #if K1R_ASM_ROUNDS
                 {
                     // the common rounds as one hand-scheduled loop (k1r_asm_rounds below)
                     uint32_t code, fx, cx;
-#if SNAPPY_K1R_ENT16
-#define e32 ent
-#define et32 ent_t
-#else
                     uint32_t e32 = ent, et32 = ent_t;
-#endif
 #ifdef SNAPPY_K1R_RSTAMPS
                     uint64_t ra0, ra1;
                     RSTAMP(ra0);
@@ -1179,22 +1088,13 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     rs_nasm++;
                     rs_code[code < 6 ? code : 0]++;
 #endif
-#if SNAPPY_K1R_ENT16
-#undef e32
-#undef et32
-#else
                     ent = (uint16_t)e32;
                     ent_t = (uint8_t)et32;
-#endif
                     if (code == 1) break;  // skip past the step-1 range, or is_block_end
                     if (code == 2) {       // the window needs to move
-#if SNAPPY_K1R_ONE_REFRESH
-                        rf = true;
-#else
                         refresh();
                         lane0 = 1;
                         if (!SNAPPY_K1R_WIN_ENT) TBL_READ_ENT(adr);
-#endif
                         continue;
                     }
                     if (code >= 4) {  // the round stopped after its inserts: finish it here
@@ -1221,13 +1121,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                         if (!(skip <= 64 - SNAPPY_K1R_LSMIN && p <= L - 16)) break;
                         lane0 = p - q0;
                         if (lane0 + SNAPPY_K1R_RMIN > 62) {
-#if SNAPPY_K1R_ONE_REFRESH
-                            rf = true;
-#else
                             refresh();
                             lane0 = 1;
                             if (!SNAPPY_K1R_WIN_ENT) TBL_READ_ENT(adr);
-#endif
                         }
                         continue;
                     }
@@ -1250,8 +1146,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 // lane l > lane0 takes the in-round candidate when its nearest same-hash lane is >= lane0 - 1;
                 // the hit test selects per lane (VALU) so one ballot carries it to SALU
                 const bool inr = (int32_t)pdl1 >= (int32_t)lane0;
-                const uint32_t hitnz = kV16 ? (inr ? pdnz : (uint32_t)ent_t) ^ ((word >> 16) & 0xFFu)
-                                                          : (inr ? pdnz : ((ent_t ^ (word >> 16)) & 0xFFu));
+                const uint32_t hitnz = (inr ? pdnz : (uint32_t)ent_t) ^ ((word >> 16) & 0xFFu);
                 const uint64_t hm = __ballot(hitnz == 0) & valid;
                 const uint32_t candv = inr ? pdc : ent;
                 const uint32_t f = (uint32_t)__builtin_ctzll(hm);
@@ -1274,9 +1169,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     const uint32_t lo0 = f > lane0 ? lane0 - 1 : lane0;
                     TBL_INSERT(lane - lo0 <= f - lo0);
                     LDS_ORDER();
-#ifndef SNAPPY_K1R_LATE_ENT
                     TBL_READ_ENT(adr);  // the next round's entries, in flight during the verification
-#endif
                     LSTAMP(s2);
                     LSEG(1, s1, s2);
                     const uint32_t pv = funnel_bytes(pa, wave_shl1(pa), perm_sel(pf & 3));
@@ -1310,9 +1203,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                         if (f == lane0) {  // its p - 1, then p again (the later write wins)
                             TBL_INSERT(lane - (lane0 - 1) <= 1);
                             LDS_ORDER();
-#ifndef SNAPPY_K1R_LATE_ENT
                             TBL_READ_ENT(adr);
-#endif
                         }
                         np = pf + ((skip + f - lane0) >> 5);
                         skip += f - lane0 + 1;
@@ -1324,9 +1215,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     // update_hash_table :303-307: p_k - 1 and p_k of every miss, lane order
                     TBL_INSERT(lane - (lane0 - 1) <= nk);
                     LDS_ORDER();
-#ifndef SNAPPY_K1R_LATE_ENT
                     TBL_READ_ENT(adr);
-#endif
                     np = q0 + lane0 + nk - 1 + ((skip + nk - 1) >> 5);  // the last probe steps by 2 at skip 64
                     skip += nk;
 #ifdef SNAPPY_K1R_STATS
@@ -1344,19 +1233,10 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 if (__builtin_expect(!(skip <= 64 - SNAPPY_K1R_LSMIN && p <= L - 16), 0)) break;
                 lane0 = p - q0;
                 if (__builtin_expect(lane0 + SNAPPY_K1R_RMIN > 62, 0)) {
-#if SNAPPY_K1R_ONE_REFRESH
-                    rf = true;
-#else
                     refresh();
                     lane0 = 1;
-#ifndef SNAPPY_K1R_LATE_ENT
                     if (!SNAPPY_K1R_WIN_ENT) TBL_READ_ENT(adr);
-#endif
-#endif
                 }
-#ifdef SNAPPY_K1R_LATE_ENT
-                TBL_READ_ENT(adr);  // every lane (reading only the probe lanes' measured 2.6 % slower)
-#endif
             }
             drain_token();
 #ifdef SNAPPY_K1R_STATS
@@ -2067,14 +1947,7 @@ __device__ __forceinline__ void k4_flush(const uint8_t *ob, uint32_t M, uint8_t 
 // source dwords: an aligned dword holding a byte of the literal never crosses
 // a page the literal does not touch), and its last min(kl, ring) bytes into the
 // ring (later copies read only that far back from the ring; further back, HBM)
-#ifndef SNAPPY_K4_LIT_INLINE
-#define SNAPPY_K4_LIT_INLINE 0
-#endif
-#if SNAPPY_K4_LIT_INLINE
-#define K4_LIT_ATTR __forceinline__
-#else
 #define K4_LIT_ATTR __noinline__
-#endif
 __device__ K4_LIT_ATTR void k4_literal_hbm(const uint8_t *lsrc, uint32_t kl, uint32_t kop, uint8_t *ob, uint32_t M,
                                                uint8_t *dst, uint32_t lane)
 {
@@ -2353,32 +2226,6 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
 #ifndef SNAPPY_K4_SPAN_ADAPT
 #define SNAPPY_K4_SPAN_ADAPT 1
 #endif
-#ifndef SNAPPY_K4_JUMP_MAX
-#define SNAPPY_K4_JUMP_MAX 1
-#endif
-#ifndef SNAPPY_K4_PACKED_SCAN
-#define SNAPPY_K4_PACKED_SCAN 1
-#endif
-// SNAPPY_K4_PASS_V2 (pass 1): a byte's address from one per-element value, kx =
-// the literal's window address - its output start, or - the copy offset: t = o +
-// kx is the window address (literal) or the source (copy); a copy overlaps its
-// own output iff t >= its start (d >= off), far iff t < lo
-#ifndef SNAPPY_K4_PASS_V2
-#define SNAPPY_K4_PASS_V2 1
-#endif
-// SNAPPY_K4_PASS_ASM (pass 1): the V2 pass as a software-pipelined asm loop
-#ifndef SNAPPY_K4_PASS_ASM
-#define SNAPPY_K4_PASS_ASM 0
-#endif
-// SNAPPY_K4_PASS_PIPE (with V2): passes software-pipelined by one stage
-#ifndef SNAPPY_K4_PASS_PIPE
-#define SNAPPY_K4_PASS_PIPE 0
-#endif
-// SNAPPY_K4_BPL4 (A/B): byte passes of 256 output bytes, four per lane (one
-// ring dword per lane, passes on 4-aligned output positions): see the pass loop
-#ifndef SNAPPY_K4_BPL4
-#define SNAPPY_K4_BPL4 0
-#endif
     // the last batch was cut by the 1,024-byte output span (long copies): parse one
     // half only -- more elements would be cut again (repeat-like data)
     bool span_cut = false;
@@ -2434,15 +2281,9 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 // exited position >= 256 (bpermute wraps addr[7:2]): one v_max per
                 // step instead of a compare and a select
                 const uint32_t J1 = 4 * lane + 4 * (size < 64 ? size : 64);
-#if SNAPPY_K4_JUMP_MAX
 #define JUMP(T, a) ({ const uint32_t _a = (a);                                            \
         const uint32_t _g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)_a, (int)(T));     \
         _g > _a ? _g : _a; })
-#else
-#define JUMP(T, a) ({ const uint32_t _a = (a);                                            \
-        const uint32_t _g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)_a, (int)(T));     \
-        _a < 256 ? _g : _a; })
-#endif
                 const uint32_t J2 = JUMP(J1, J1);
                 const uint32_t J4 = JUMP(J2, J2);
                 const uint32_t J8 = JUMP(J4, J4);
@@ -2530,7 +2371,6 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
         // exclusive prefix sums of compressed sizes and output lengths over
         // the batch (64-bit safe: garbage past E is zeroed)
         const bool live = lane < E;
-#if SNAPPY_K4_PACKED_SCAN
         // both scans as one over size | len << 16, each clamped to 1,023: exact for
         // every lane, because only the batch's last element can exceed 440 in either
         // (an element followed by another of its half is < 64 bytes; one that ends a
@@ -2545,11 +2385,6 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             in_off = ex & 0xFFFF;
             out_off = ex >> 16;
         }
-#else
-        uint32_t tot_in, tot_out;
-        const uint32_t in_off = wave_excl_scan(live ? e_size : 0, lane, &tot_in);
-        const uint32_t out_off = wave_excl_scan(live ? e_len : 0, lane, &tot_out);
-#endif
         // validity in stream order: stop at the first element that runs past the
         // unit (truncated / overrun), reaches before the stream start, or needs
         // an earlier unit's bytes (pass 1: DEFER); an element running past the
@@ -2642,9 +2477,8 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             // op_end) too: a batch starts with op - F < kK4FlushAt (the flush below),
             // and kK4FlushAt + kK4MapBits <= ring - 64
             static_assert(kK4FlushAt + kK4MapBits <= kK4Ring - 64, "K4: the ring must hold [F, op_end)");
-            // (four bytes per lane: the map starts at op & ~3, so op & 3 bits fewer)
             const uint64_t over = __ballot(lane < nexec && lane > 0 &&
-                                           out_off + e_len > kK4MapBits - (SNAPPY_K4_BPL4 ? (op & 3) : 0u));
+                                           out_off + e_len > kK4MapBits);
 #ifdef SNAPPY_K4_STATS
             const uint32_t nexec_l = nexec;
 #endif
@@ -2691,10 +2525,9 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             // LDS operations complete in issue order, so only the compiler could
             // reorder the clear, the or and the read; lanes w and w + 32 store
             // the same zero into dword w)
-            const uint32_t mh = SNAPPY_K4_BPL4 ? (op & 3) : 0u;  // the map's bit 0 = output byte op - mh
             map32[lane & 31] = 0;
             asm volatile("" ::: "memory");
-            if (ex) __hip_atomic_fetch_or(map32 + ((out_off + mh) >> 5), 1u << ((out_off + mh) & 31), __ATOMIC_RELAXED,
+            if (ex) __hip_atomic_fetch_or(map32 + (out_off >> 5), 1u << (out_off & 31), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WORKGROUP);
             asm volatile("" ::: "memory");
             const uint32_t bm = map32[lane & 31];
@@ -2705,372 +2538,14 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
             // 32 KiB streams and 1.3 % on 64 KiB blocks: profiles/r04a_ab_k4_*, r04b_ab_k4_*)
             const uint32_t kop = e_op | (e_t == 0 ? 0x80000000u : 0u);
             const uint32_t kinfo = e_t == 0 ? (256 * ws + e_lsrc) ^ 0x80000000u : e_info;
-#if SNAPPY_K4_BPL4
-            // four output bytes per lane: pass P covers [P, P + 256) from P0 = op & ~3,
-            // lane l owns ring dword (P + 4l) & M.  Bytes below op and from op_end on
-            // are kept (written back with the ring's own value).  A byte's element:
-            // the starts before the lane's first byte (whole map dwords below, by one
-            // scan per batch, + the bits below it in its dword) and those in its
-            // nibble.  Elements of bytes 0 and 1 are e0 or e0 + 1, looked up for every
-            // lane; bytes 2 and 3 of a lane with two or more starts in bytes 1..3 look
-            // theirs up (a uniform branch on the ballot)
-            const uint32_t P0 = op - mh;
-            const uint32_t pcn = (uint32_t)__builtin_popcount(bm);  // lanes >= 32 repeat 0..31
-            uint32_t cx = pcn;
-            cx += dpp0<0x111, 0xF>(cx);
-            cx += dpp0<0x112, 0xF>(cx);
-            cx += dpp0<0x114, 0xF>(cx);
-            cx += dpp0<0x118, 0xF>(cx);
-            cx += dpp0<0x142, 0xA>(cx);
-            cx -= pcn;  // lanes 0..31: the starts in map dwords below the lane's
-            const uint32_t nsh = 4 * (lane & 7);
-            const uint32_t lmask = (1u << nsh) - 1;
-            for (uint32_t P = P0, i = 0; P < op_end; P += 256, i++) {
-                const int wa = (int)(4 * (8 * i + (lane >> 3)));
-                const uint32_t dw = (uint32_t)__builtin_amdgcn_ds_bpermute(wa, (int)bm);
-                const uint32_t cnt = (uint32_t)__builtin_amdgcn_ds_bpermute(wa, (int)cx);
-                const uint32_t nib = (dw >> nsh) & 15;
-                const uint32_t e0 = (uint32_t)__builtin_popcount(dw & lmask) + cnt + (nib & 1) - 1;
-                const uint32_t F0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(e0 << 2), (int)kop);
-                const uint32_t I0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(e0 << 2), (int)kinfo);
-                const uint32_t F1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((e0 + 1) << 2), (int)kop);
-                const uint32_t I1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((e0 + 1) << 2), (int)kinfo);
-                const bool multi = __ballot(__builtin_popcount(nib & 14) >= 2) != 0;
-                const uint32_t o0 = P + 4 * lane;
-                uint32_t wv = 0;
-                SrcT srcb[4];
-                bool inp[4];
-#pragma unroll
-                for (uint32_t b = 0; b < 4; b++) {
-                    const uint32_t o = o0 + b;
-                    const uint32_t kb = (uint32_t)__builtin_popcount(nib & (14u & ((2u << b) - 1)));
-                    uint32_t f_op = kb ? F1 : F0, f_in = kb ? I1 : I0;
-                    if (b >= 2 && multi) {
-                        const int ea = (int)((e0 + kb) << 2);
-                        const uint32_t g_op = (uint32_t)__builtin_amdgcn_ds_bpermute(ea, (int)kop);
-                        const uint32_t g_in = (uint32_t)__builtin_amdgcn_ds_bpermute(ea, (int)kinfo);
-                        f_op = kb >= 2 ? g_op : f_op;
-                        f_in = kb >= 2 ? g_in : f_in;
-                    }
-                    const uint32_t d = o - f_op;  // a literal's carries 2^31, cancelled by its kinfo
-                    const bool lit = (int32_t)f_op < 0;
-                    const bool pend = o >= op && o < op_end;
-                    SrcT src = (SrcT)o - (SrcT)f_in;
-                    bool far = pend && !lit && src < (SrcT)lo;
-                    uint32_t fv = 0;
-#ifndef SNAPPY_K4_NOFAR
-                    if (far) fv = dst[src];
-#endif
-                    uint32_t a = f_in + d;
-                    const uint32_t a2 = a - 768;
-                    a = a < a2 ? a : a2;
-                    const uint32_t lb = wb[a < 783 ? a : 783];
-                    if (pend && !lit && !far && d >= f_in) {
-                        // overlapping copy (off < len <= 64): source byte d mod off
-                        const float r = __builtin_amdgcn_rcpf((float)f_in);
-                        const uint32_t qd = (uint32_t)((float)d * r + 0.0001f);
-                        src = (SrcT)f_op - (SrcT)f_in + (SrcT)(d - qd * f_in);
-                        if constexpr (BACK) {
-                            if (src < (SrcT)lo) {
-                                fv = dst[src];
-                                far = true;
-                            }
-                        }
-                    }
-#ifdef SNAPPY_K4_STATS
-                    n_far += (b == 0 && __ballot(far) != 0) ? 1u : 0u;
-#endif
-                    inp[b] = pend && !lit && !far && src >= (SrcT)P;
-                    srcb[b] = pend ? src : (SrcT)o;
-                    const uint8_t rv = ob[(uint32_t)srcb[b] & M];
-                    const uint8_t lr = (pend && lit) ? (uint8_t)lb : rv;
-                    const uint32_t v = far ? fv : (uint32_t)lr;
-                    wv |= (v & 0xFF) << (8 * b);
-                }
-                auto *const od = reinterpret_cast<uint32_t *>(ob + (o0 & M));
-                *od = wv;
-#ifdef SNAPPY_K4_STATS
-                n_pass++;
-                n_sub++;
-#endif
-                if (__builtin_expect(__ballot(inp[0] || inp[1] || inp[2] || inp[3]) != 0, 0)) {
-                    // sources inside this pass (each below its byte: a copy's source, mapped
-                    // mod off for overlapping copies, lies before the copy): re-read them
-                    // until nothing changes.  Every round reads what the last one wrote
-                    // (one wave's LDS operations complete in order), and the only fixed
-                    // point of an acyclic system is its solution
-                    for (;;) {
-                        uint32_t nv = wv;
-#pragma unroll
-                        for (uint32_t b = 0; b < 4; b++) {
-                            const uint32_t r = ob[(uint32_t)srcb[b] & M];
-                            nv = inp[b] ? ((nv & ~(0xFFu << (8 * b))) | (r << (8 * b))) : nv;
-                        }
-#ifdef SNAPPY_K4_STATS
-                        n_sub++;
-#endif
-                        if (!__ballot(nv != wv)) break;
-                        *od = nv;
-                        wv = nv;
-                    }
-                }
-            }
-#else
             uint32_t cb = 0;  // elements starting before the pass
-#if SNAPPY_K4_PASS_ASM
             if constexpr (!BACK) {
-            // the V2 pass (below) as one hand-scheduled asm loop, software-pipelined by
-            // one stage: the element lookup of pass i + 1 (bitmap read-back, mbcnt, the
-            // two ds_bpermute) is issued before pass i waits for its window / ring bytes,
-            // and its far load (a copy source older than the ring, from HBM) and window
-            // read before pass i + 1 begins, so each wait covers one pass's latency
-            // instead of the compiler's lgkmcnt(0) / vmcnt(0) after every load
-            // (DESIGN.md 4.3).  Every wait is written out: LDS operations complete in
-            // issue order (lgkmcnt(N) = all but the N youngest), the far load is the
-            // only vector-memory operation in flight.  Wait states: a VALU-written mask
-            // is read by VALU >= 2 instructions later, v_rcp's result 1 later.  exec is
-            // saved and restored around every masked region.  vcc carries the pass's
-            // 64 bitmap bits (lo / hi halves are nameable).  Output bytes, ring and
-            // window addresses are those of the V2 loop; the LDS array starts at
-            // address 0 (checked below), so window bytes are at 0 + t and the ring at
-            // kK4RingAt + (x & M).
-            const uint32_t kx = e_t == 0 ? 256 * ws + e_lsrc - e_op : 0u - e_info;
-            if (__builtin_expect((uint32_t)(uintptr_t)wb != 0, 0)) __builtin_trap();
-            uint32_t sP, si2, scb, sA, sB, sF;
-            uint64_t mp, ml, mf, mc, mo, sv;
-            uint32_t vo, vt, vfo, vfx, vfv, vlb, vrv, vva, vtm, vtn;
-#define K4A1                                                                                         \
-    "s_add_u32 %[sA], %[i2], 1\n\t"                                                                \
-    "v_readlane_b32 vcc_lo, %[bm], %[i2]\n\t" /* (an SALU-written lane select: one apart) */        \
-    "v_readlane_b32 vcc_hi, %[bm], %[sA]\n\t"                                                      \
-    "s_and_b32 %[sA], vcc_lo, 1\n\t"                                                               \
-    "s_add_u32 %[sA], %[sA], %[cb]\n\t"                                                            \
-    "s_sub_u32 %[sA], %[sA], 1\n\t" /* cb - 1 + (sm & 1) */                                        \
-    "s_bcnt1_i32_b64 %[sB], vcc\n\t"                                                               \
-    "s_add_u32 %[cb], %[cb], %[sB]\n\t"                                                            \
-    "s_lshr_b64 vcc, vcc, 1\n\t"                                                                   \
-    "v_mov_b32 %[vtm], %[sA]\n\t"                                                                  \
-    "v_mbcnt_lo_u32_b32 %[vtm], vcc_lo, %[vtm]\n\t"                                                \
-    "v_mbcnt_hi_u32_b32 %[vtm], vcc_hi, %[vtm]\n\t" /* the byte's element */                       \
-    "v_lshlrev_b32 %[vtm], 2, %[vtm]\n\t"                                                          \
-    "ds_bpermute_b32 %[vfo], %[vtm], %[kop]\n\t"                                                   \
-    "ds_bpermute_b32 %[vfx], %[vtm], %[kx]\n\t"                                                    \
-    "s_add_u32 %[i2], %[i2], 2\n\t"
-#define K4A2                                                                                         \
-    "v_cmp_gt_u32_e64 %[mp], %[opend], %[vo]\n\t" /* pend */                                       \
-    "v_cmp_gt_i32_e64 %[ml], 0, %[vfo]\n\t"       /* literal */                                    \
-    "v_add_u32_e32 %[vt], %[vo], %[vfx]\n\t"      /* window address or copy source */              \
-    "v_cmp_gt_u32_e64 %[mf], %[lo], %[vt]\n\t"                                                     \
-    "s_andn2_b64 %[mf], %[mf], %[ml]\n\t"                                                          \
-    "s_and_b64 %[mf], %[mf], %[mp]\n\t"           /* far: older than the ring */                   \
-    "s_and_saveexec_b64 %[sv], %[mf]\n\t"                                                          \
-    "global_load_ubyte %[vfv], %[vt], %[dst]\n\t"                                                  \
-    "s_mov_b64 exec, %[sv]\n\t"                                                                    \
-    "v_add_u32_e32 %[vtn], 0xfffffd00, %[vt]\n\t"                                                  \
-    "v_min3_u32 %[vtn], %[vt], %[vtn], %[wmax]\n\t"                                                \
-    "ds_read_u8 %[vlb], %[vtn]\n\t"               /* the window byte */
-            if (op < op_end) {
-                asm volatile(
-                    "s_mov_b32 %[P], %[op]\n\t"
-                    "s_mov_b32 %[i2], 0\n\t"
-                    "s_mov_b32 %[cb], 0\n\t"
-                    "v_add_u32_e32 %[vo], %[op], %[lane]\n\t"
-                    K4A1
-                    "s_waitcnt lgkmcnt(0)\n\t"
-                    K4A2
-                    "L%=_top:\n\t"
-                    // ---- pass P, stage B: an overlapping copy's source (byte d mod off)
-                    "s_or_b64 %[mc], %[ml], %[mf]\n\t"
-                    "s_andn2_b64 %[mc], %[mp], %[mc]\n\t"      /* copy from the ring */
-                    "v_cmp_ge_u32_e64 %[mo], %[vt], %[vfo]\n\t"
-                    "s_and_b64 %[mo], %[mo], %[mc]\n\t"
-                    "s_cbranch_scc0 L%=_noov\n\t"
-                    "s_and_saveexec_b64 %[sv], %[mo]\n\t"
-                    "v_sub_u32_e32 %[vtn], 0, %[vfx]\n\t"      /* off */
-                    "v_cvt_f32_u32_e32 %[vtn], %[vtn]\n\t"
-                    "v_sub_u32_e32 %[vtm], %[vo], %[vfo]\n\t"  /* d */
-                    "v_cvt_f32_u32_e32 %[vtm], %[vtm]\n\t"
-                    "v_rcp_f32_e32 %[vtn], %[vtn]\n\t"
-                    "s_nop 0\n\t"
-                    "v_fmaak_f32 %[vtm], %[vtn], %[vtm], 0x38d1b717\n\t"  /* d / off + 1e-4 */
-                    "v_cvt_u32_f32_e32 %[vtm], %[vtm]\n\t"
-                    "v_mad_i32_i24 %[vt], %[vtm], %[vfx], %[vt]\n\t"       /* t - qd * off */
-                    "s_mov_b64 exec, %[sv]\n"
-                    "L%=_noov:\n\t"
-                    "v_and_b32_e32 %[vtm], 0xfff, %[vt]\n\t"
-                    "ds_read_u8 %[vrv], %[vtm] offset:%[ringat]\n\t"     /* the ring byte */
-                    "v_cmp_ge_u32_e64 %[mo], %[vt], %[P]\n\t"
-                    "s_and_b64 %[mo], %[mo], %[mc]\n\t"        /* a source inside this pass */
-                    "s_cselect_b32 %[sF], 1, 0\n\t"
-                    // ---- pass P + 64, stage A (element lookup)
-                    K4A1
-                    "s_waitcnt lgkmcnt(2)\n\t"                 /* window and ring bytes of pass P */
-                    "s_waitcnt vmcnt(0)\n\t"                   /* its far bytes */
-                    "v_cndmask_b32_e64 %[vva], %[vrv], %[vlb], %[ml]\n\t"
-                    "v_cndmask_b32_e64 %[vva], %[vva], %[vfv], %[mf]\n\t"
-                    "s_cmp_lg_u32 %[sF], 0\n\t"
-                    "s_cbranch_scc1 L%=_inpass\n"
-                    "L%=_write:\n\t"
-                    "v_and_b32_e32 %[vtm], 0xfff, %[vo]\n\t"
-                    "s_and_saveexec_b64 %[sv], %[mp]\n\t"
-                    "ds_write_b8 %[vtm], %[vva] offset:%[ringat]\n\t"
-                    "s_mov_b64 exec, %[sv]\n\t"
-                    "s_add_u32 %[P], %[P], 64\n\t"
-                    "s_cmp_ge_u32 %[P], %[opend]\n\t"
-                    "s_cbranch_scc1 L%=_exit\n\t"
-                    // ---- pass P + 64, stage A (its bytes' sources)
-                    "v_add_u32_e32 %[vo], 64, %[vo]\n\t"
-                    "s_waitcnt lgkmcnt(1)\n\t"                 /* its two bpermutes (the write may pend) */
-                    K4A2
-                    "s_branch L%=_top\n"
-                    // ---- rare: sources inside the pass, by pointer jumping over lanes
-                    "L%=_inpass:\n\t"
-                    "v_subrev_u32_e32 %[vtm], %[P], %[vt]\n\t"
-                    "v_cndmask_b32_e64 %[vtm], %[lane], %[vtm], %[mo]\n"
-                    "L%=_pj:\n\t"
-                    "v_lshlrev_b32_e32 %[vtn], 2, %[vtm]\n\t"
-                    "ds_bpermute_b32 %[vfv], %[vtn], %[vtm]\n\t"
-                    "s_waitcnt lgkmcnt(0)\n\t"
-                    "v_cmp_ne_u32_e64 %[mo], %[vfv], %[vtm]\n\t"
-                    "v_mov_b32_e32 %[vtm], %[vfv]\n\t"
-                    "s_cmp_lg_u64 %[mo], 0\n\t"
-                    "s_cbranch_scc1 L%=_pj\n\t"
-                    "v_lshlrev_b32_e32 %[vtn], 2, %[vtm]\n\t"
-                    "ds_bpermute_b32 %[vva], %[vtn], %[vva]\n\t"
-                    "s_waitcnt lgkmcnt(0)\n\t"
-                    "s_branch L%=_write\n"
-                    "L%=_exit:\n\t"
-                    "s_waitcnt lgkmcnt(0)"
-                    : [P] "=&s"(sP), [i2] "=&s"(si2), [cb] "=&s"(scb), [sA] "=&s"(sA), [sB] "=&s"(sB),
-                      [sF] "=&s"(sF), [mp] "=&s"(mp), [ml] "=&s"(ml), [mf] "=&s"(mf), [mc] "=&s"(mc),
-                      [mo] "=&s"(mo), [sv] "=&s"(sv), [vo] "=&v"(vo), [vt] "=&v"(vt), [vfo] "=&v"(vfo),
-                      [vfx] "=&v"(vfx), [vfv] "=&v"(vfv), [vlb] "=&v"(vlb), [vrv] "=&v"(vrv), [vva] "=&v"(vva),
-                      [vtm] "=&v"(vtm), [vtn] "=&v"(vtn)
-                    : [bm] "v"(bm), [kop] "v"(kop), [kx] "v"(kx), [lane] "v"(lane), [op] "s"(op),
-                      [opend] "s"(op_end), [lo] "s"(lo), [dst] "s"(dst), [wmax] "s"(783u), [ringat] "i"(kK4RingAt)
-                    : "vcc", "scc", "memory");
-            }
-#undef K4A1
-#undef K4A2
-            } else
-#elif SNAPPY_K4_PASS_V2 && SNAPPY_K4_PASS_PIPE
-            if constexpr (!BACK) {
-            const uint32_t kx = e_t == 0 ? 256 * ws + e_lsrc - e_op : 0u - e_info;
-            // software-pipelined passes: stage A of pass i + 1 (element lookup, address,
-            // far load, window byte -- nothing that reads the ring) is issued before stage
-            // B of pass i (ring read, in-pass fix-up, ring write), so its LDS and memory
-            // latencies overlap pass i's work (K4 runs ~8 % slower per wave removed
-            // from a SIMD: it is latency-bound, profiles/r05s_ab_kb-k4o7-k4o6_*)
-            struct PassA {
-                uint32_t f_op, t, lb, fv;
-                bool lit, pend, far;
-            };
-            auto stage_a = [&](uint32_t P, uint32_t i, PassA &s) {
-                const uint64_t sm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(bm, 2 * i + 1) << 32) |
-                                    (uint32_t)__builtin_amdgcn_readlane(bm, 2 * i);
-                const uint64_t sm1 = sm >> 1;
-                const uint32_t id = __builtin_amdgcn_mbcnt_hi(
-                    (uint32_t)(sm1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm1, cb - 1 + (uint32_t)(sm & 1)));
-                cb += (uint32_t)__builtin_popcountll(sm);
-                s.f_op = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)kop);
-                const uint32_t f_x = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)kx);
-                const uint32_t o = P + lane;
-                s.lit = (int32_t)s.f_op < 0;
-                s.pend = o < op_end;
-                uint32_t t = o + f_x;
-                s.far = s.pend && !s.lit && t < lo;
-#if SNAPPY_K4_PASS_PIPE == 2
-                // every lane loads (a lane that is not far reads dst[0]: one line), so
-                // the load is straight-line code whose wait the compiler can count
-                s.fv = dst[s.far ? t : 0u];
-#else
-                asm volatile("" : "=v"(s.fv));  // (no initial value: read only where far)
-#ifndef SNAPPY_K4_NOFAR
-                if (s.far) s.fv = dst[t];
-#endif
-#endif
-                const uint32_t a2 = t - 768;
-                s.lb = wb[__builtin_elementwise_min(__builtin_elementwise_min(t, a2), 783u)];
-                if (s.pend && !s.lit && !s.far && t >= s.f_op) {
-                    const uint32_t off = 0u - f_x, d = o - s.f_op;
-                    const float r = __builtin_amdgcn_rcpf((float)off);
-                    const uint32_t qd = (uint32_t)((float)d * r + 0.0001f);
-                    t = s.f_op - off + (d - qd * off);
-                }
-                s.t = t;
-            };
-            PassA cur, nxt;
-#if SNAPPY_K4_PASS_PIPE == 2
-            // ping-pong (no register copies of in-flight loads at the loop latch)
-            auto stage_b = [&](uint32_t P, const PassA &c) {
-                const uint32_t o = P + lane;
-                const int32_t tin = (c.pend && !c.lit && !c.far) ? (int32_t)c.t : -1;
-                const uint8_t rv = ob[c.t & M];
-                const uint8_t lr = c.lit ? (uint8_t)c.lb : rv;
-                uint32_t val = c.far ? c.fv : (uint32_t)lr;
-                if (__builtin_expect(__ballot(tin >= (int32_t)P) != 0, 0)) {
-                    uint32_t rt = tin >= (int32_t)P ? c.t - P : lane;
-                    for (;;) {
-                        const uint32_t r2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rt << 2), (int)rt);
-                        if (!__ballot(r2 != rt)) break;
-                        rt = r2;
-                    }
-                    val = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rt << 2), (int)val);
-                }
-                ob[c.pend ? (o & M) : kK4Ring] = (uint8_t)val;
-            };
-            PassA sa, sb;
-            stage_a(op, 0, sa);
-            for (uint32_t P = op, i = 0;;) {
-                const bool m1 = P + 64 < op_end;
-                if (m1) stage_a(P + 64, i + 1, sb);
-                stage_b(P, sa);
-                if (!m1) break;
-                P += 64;
-                i++;
-                const bool m2 = P + 64 < op_end;
-                if (m2) stage_a(P + 64, i + 1, sa);
-                stage_b(P, sb);
-                if (!m2) break;
-                P += 64;
-                i++;
-            }
-            if (false)
-#else
-            stage_a(op, 0, cur);
-#endif
-            for (uint32_t P = op, i = 0; P < op_end; P += 64, i++) {
-                if (P + 64 < op_end) stage_a(P + 64, i + 1, nxt);
-                const uint32_t o = P + lane;
-#ifdef SNAPPY_K4_STATS
-                n_far += __ballot(cur.far) != 0;
-                n_pass++;
-#endif
-                const int32_t tin = (cur.pend && !cur.lit && !cur.far) ? (int32_t)cur.t : -1;
-                const uint8_t rv = ob[cur.t & M];
-                const uint8_t lr = cur.lit ? (uint8_t)cur.lb : rv;
-                uint32_t val = cur.far ? cur.fv : (uint32_t)lr;
-                if (__builtin_expect(__ballot(tin >= (int32_t)P) != 0, 0)) {
-                    uint32_t rt = tin >= (int32_t)P ? cur.t - P : lane;
-                    for (;;) {
-#ifdef SNAPPY_K4_STATS
-                        n_sub++;
-#endif
-                        const uint32_t r2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rt << 2), (int)rt);
-                        if (!__ballot(r2 != rt)) break;
-                        rt = r2;
-                    }
-                    val = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rt << 2), (int)val);
-                }
-                ob[cur.pend ? (o & M) : kK4Ring] = (uint8_t)val;
-#ifdef SNAPPY_K4_STATS
-                n_sub++;
-#endif
-                cur = nxt;
-            }
-            } else
-#elif SNAPPY_K4_PASS_V2
-            if constexpr (!BACK) {
+            // pass 1: a byte's address from one per-element value, kx = the literal's
+            // window address - its output start, or - the copy offset: t = o + kx is the
+            // window address (literal) or the source (copy); a copy overlaps its own
+            // output iff t >= its start (d >= off), far iff t < lo.  (A software-
+            // pipelined asm form of this loop, with every wait written out and four
+            // VALU fewer per pass, measured the same: DESIGN.md 4.3.)
             const uint32_t kx = e_t == 0 ? 256 * ws + e_lsrc - e_op : 0u - e_info;
             for (uint32_t P = op, i = 0; P < op_end; P += 64, i++) {
                 const uint64_t sm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(bm, 2 * i + 1) << 32) |
@@ -3129,7 +2604,6 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
 #endif
             }
             } else
-#endif
             // pass P: byte lane l writes output byte o = P + l
             for (uint32_t P = op, i = 0; P < op_end; P += 64, i++) {
                 const uint64_t sm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(bm, 2 * i + 1) << 32) |
@@ -3212,7 +2686,6 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 n_sub++;
 #endif
             }
-#endif
         }
         K4STAMP(td);
 #ifdef SNAPPY_K4_STATS
@@ -4091,7 +3564,7 @@ extern "C" __attribute__((visibility("hidden"))) const char *snappy_amd_config_d
 #else
            " k4_nofar=0"
 #endif
-           " k4_bpl4=" CFG_STR(SNAPPY_K4_BPL4) " k4_pass_pipe=" CFG_STR(SNAPPY_K4_PASS_PIPE) "}";
+           "}";
 }
 #endif
 

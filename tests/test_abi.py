@@ -101,8 +101,7 @@ def assert_product_config(cfg: str):
     """A shipped library: both kernel halves built without measurement knobs
     (the wrong-output ones cannot even compile without SNAPPY_MEASUREMENT_BUILD)."""
     assert cfg.startswith("compress{") and " decode{" in cfg, cfg
-    for must in ("compress{measurement=0", "decode{measurement=0", "k2_nolit=0", "k4_nofar=0", "k1r_asm=1",
-                 "k4_bpl4=0", "k4_pass_pipe=0"):
+    for must in ("compress{measurement=0", "decode{measurement=0", "k2_nolit=0", "k4_nofar=0", "k1r_asm=1"):
         assert must in cfg, (must, cfg)
 
 

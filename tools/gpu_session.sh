@@ -186,6 +186,15 @@ for step in "$@"; do
         IFS=: read -r _ chunk <<< "$step"
         timeout -k 10 200 python -u tools/k1r_rstamps.py 268435456 $chunk rst > "$out/rst_$chunk.log" 2>&1
         rc=$?; echo "rst rc=$rc"; cat "$out/rst_$chunk.log"; [ $rc -ne 0 ] && exit $rc ;;
+    prof1m)  # configs[0]'s 1,000,000-byte compress alone: K1r64 over 16 blocks = one lone wave's chain
+        timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$out/prof1m" -o run --output-format csv -- \
+            python3 tools/run_once.py T 1000000 65536 > "$out/prof1m.log" 2>&1
+        rc=$?; echo "prof1m rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
+    tracee2e)  # kernel trace of the end-to-end pipeline over a 1-rank RCCL communicator (C2 beside K1r?)
+        timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$out/tracee2e" -o run --output-format csv -- \
+            python3 bench.py --dist-world1 --dist-backend nccl --total-bytes 8589934592 --steps 1 --warmup 1 \
+            --e2e-steps 1 --no-sub --no-cpu-baseline --no-host-e2e > "$out/tracee2e.log" 2>&1
+        rc=$?; echo "tracee2e rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -51,6 +51,8 @@ for w in sorted(os.listdir(src)):
     fetch = per_kernel(os.path.join(d, "fetch", "run_counter_collection.csv"))
     write = per_kernel(os.path.join(d, "write", "run_counter_collection.csv"))
     sq = per_kernel(os.path.join(d, "sq", "run_counter_collection.csv"))
+    for k, cs in per_kernel(os.path.join(d, "sq2", "run_counter_collection.csv")).items():
+        sq.setdefault(k, {}).update({c: v for c, v in cs.items() if c != "SQ_WAVES"})
     n = line["config"]["bytes_per_gpu"]
     # bench.py matches a summary to its line by workload and launch size
     res = {"label": w, "workload": line["config"].get("workload_name", w), "bytes_per_gpu": n,
@@ -67,9 +69,27 @@ for w in sorted(os.listdir(src)):
         for c, v in sorted(sq.get(k, {}).items()):
             e[c] = round(v)
         if e.get("SQ_WAVES"):
-            for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"):
+            for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD"):
                 if c in e:
                     e[c + "_per_wave"] = round(e[c] / e["SQ_WAVES"], 1)
+            # busy fractions: the counters are quad-cycles summed over
+            # waves, so a per-SIMD fraction is waves-per-SIMD x per-wave count / per-wave
+            # SQ_WAVE_CYCLES; waves per SIMD from the kernel's occupancy
+            occ = {"k1r_match_units": 3, "k1r_match_units64": 3, "k4_decompress_units": 8, "k2_emit_units": 6}.get(k)
+            wc = e.get("SQ_WAVE_CYCLES", 0) / e["SQ_WAVES"]
+            if occ and wc:
+                frac = {}
+                for c, name in (("SQ_ACTIVE_INST_VALU", "simd_valu_active"), ("SQ_ACTIVE_INST_SCA", "simd_salu_active"),
+                                ("SQ_ACTIVE_INST_LDS", "simd_lds_inst_active")):
+                    if c in e:
+                        frac[name] = round(occ * e[c] / e["SQ_WAVES"] / wc, 3)
+                for c, name in (("SQ_WAIT_ANY", "wave_waitcnt_parked"), ("SQ_WAIT_INST_ANY", "wave_issue_stalled"),
+                                ("SQ_ACTIVE_INST_ANY", "wave_issuing"), ("SQ_WAIT_INST_LDS", "wave_lds_issue_stalled")):
+                    if c in e:
+                        frac[name] = round(e[c] / e["SQ_WAVES"] / wc, 3)
+                frac["waves_per_simd"] = occ
+                frac["wave_cycles_per_wave"] = round(4 * wc)
+                e["busy"] = frac
         res["kernels"][k] = e
     for name in (f"{rnd}_{w}_pmc.json", f"pmc_{w}.json"):
         json.dump(res, open(os.path.join(out, name), "w"), indent=1)

@@ -7,7 +7,8 @@
 #   bench.json    the bench.py line (CPU baselines on a bounded sample)
 #   trace/        rocprofv3 --kernel-trace --stats of the same command
 #   fetch/ write/ rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE (separate passes, kernel trace only)
-#   sq/           rocprofv3 --pmc of 8 SQ counters (instruction mix, wave cycles)
+#   sq/ sq2/      rocprofv3 --pmc of 8 + 8 SQ counters (instruction mix, wave cycles,
+#                 issue / wait / LDS cycles: the busy fractions of DESIGN.md 4.2-4.3)
 # tools/pmc_summary.py then writes profiles/<round>_W_*.  Every GPU step has its
 # own time limit; steps are chained with && so the first failure ends the run.
 set -o pipefail
@@ -15,7 +16,8 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 WLS=${*:-"config3 text32k text64k random repeat decode10g"}
 STEPS=${STEPS:-5}
-SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"
+SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_SCA SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"
+SQ2="SQ_WAVES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD"
 run() {  # workload
     # --no-sub: the profiled process runs this workload only (the default line also runs the
     # other configs, whose launches of the same kernels would be averaged into W's counters)
@@ -41,7 +43,10 @@ run() {  # workload
         python3 bench.py $q --steps 2 --warmup 1 > $d/write.log 2>&1 &&
     echo "[$(date +%T)] $w: SQ counters" &&
     timeout -k 10 400 rocprofv3 --pmc $SQ --kernel-trace -d $d/sq -o run --output-format csv -- \
-        python3 bench.py $q --steps 2 --warmup 1 > $d/sq.log 2>&1
+        python3 bench.py $q --steps 2 --warmup 1 > $d/sq.log 2>&1 &&
+    echo "[$(date +%T)] $w: SQ counters, pass 2" &&
+    timeout -k 10 400 rocprofv3 --pmc $SQ2 --kernel-trace -d $d/sq2 -o run --output-format csv -- \
+        python3 bench.py $q --steps 2 --warmup 1 > $d/sq2.log 2>&1
 }
 for w in $WLS; do
     run $w || exit 1

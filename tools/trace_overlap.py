@@ -68,6 +68,25 @@ def main():
         res["rccl_total_ms"] = round(tot / 1e6, 3)
         res["rccl_overlap_fraction"] = round(ov / tot, 3) if tot else None
         res["rccl_queues_disjoint_from_k1r"] = not (fam["rccl"]["queues"] & fam["k1r_match_units"]["queues"])
+    # every (queue, stream, kernel family) against K1r's launches: at world 1 RCCL's
+    # all-gather is a copy kernel on the process group's own stream, so the copy
+    # kernels are listed per queue / stream as well
+    if "k1r_match_units" in fam:
+        k = merge(fam["k1r_match_units"]["iv"])
+        per = {}
+        for r in rows:
+            n = r["Kernel_Name"]
+            f = family(n)
+            if f == "other":
+                f = n.split("(")[0].split("<")[0].replace("void ", "")[:48]
+            key = f"q{r['Queue_Id']}/s{r.get('Stream_Id') or 0}/{f}"
+            per.setdefault(key, []).append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+        res["vs_k1r"] = {}
+        for key, iv in sorted(per.items()):
+            m = merge(iv)
+            tot = sum(b - a for a, b in m)
+            res["vs_k1r"][key] = {"launches": len(iv), "busy_ms": round(tot / 1e6, 3),
+                                  "during_k1r_ms": round(overlap(m, k) / 1e6, 3)}
     print(json.dumps(res, indent=1))
     if len(sys.argv) > 2:
         json.dump(res, open(sys.argv[2], "w"), indent=1)

@@ -278,22 +278,25 @@ __device__ __forceinline__ uint32_t tconf(uint32_t h, uint32_t a, uint32_t notdu
 }
 
 #ifndef SNAPPY_K1R_DMAX
-#define SNAPPY_K1R_DMAX 10  // lane-space rounds: same-hash distances resolved per window (8/10/12/14/16
-                            // measured, profiles/r03h_ab_k1r_dmax_rmin_*; after the early entry read
-                            // 9 / 10 / 12: 16.07 / 16.19 / 16.18 ms per GiB, profiles/r03s2z_*, r03s2aa_*;
-                            // with the round-5 asm loop, each at its best loop placement, 8 / 9 / 10:
-                            // 12.46 / 12.37 / 12.23 ms per GiB, profiles/r05zw_*)
+#define SNAPPY_K1R_DMAX 13  // lane-space rounds: same-hash distances resolved per window (8/10/12/14/16
+                            // measured, profiles/r03h_ab_k1r_dmax_rmin_*; with the round-5 asm loop at
+                            // its best loop placement 8 / 9 / 10: 12.46 / 12.37 / 12.23 ms per GiB,
+                            // profiles/r05zw_*; round 6 at RMIN 2: 11 / 13 / 14 / 16 -> 12.31-12.32 /
+                            // 12.26-12.27 / 12.34-12.37 / 12.52-12.58, profiles/r06m_*)
 #endif
 #ifndef SNAPPY_K1R_DMAX64
-#define SNAPPY_K1R_DMAX64 9  // K1r64 (65,536-byte blocks), with the asm round loop: 9 / 10 / 11 / 12 -> 18.70-18.73 / 18.81-18.82 / 18.75 / 18.81-18.84 ms
+#define SNAPPY_K1R_DMAX64 12  // K1r64 (65,536-byte blocks): round 6 at RMIN 2, 10 / 12 / 13 / 14 ->
+                              // 14.07-14.09 / 14.03-14.04 / 14.42 / 14.12-14.13 ms per GiB (r06m_*)
 #endif
 #ifndef SNAPPY_K1R_LSMIN
 #define SNAPPY_K1R_LSMIN 4  // lane-space rounds while at least this many step-1 probes remain
 #endif
 #ifndef SNAPPY_K1R_RMIN
-#define SNAPPY_K1R_RMIN 6  // refresh the window when fewer probe lanes remain (6 / 8 / 10 after the
-                           // early entry read: 16.14 / 16.19 / 16.26 ms per GiB, 64 KiB blocks
-                           // 19.15 / 19.23 / 19.30; profiles/r03s2z_*)
+#define SNAPPY_K1R_RMIN 2  // refresh the window when fewer probe lanes remain (round 6, DMAX 13 / 12:
+                           // 1 / 2 / 3 / 4 / 6 -> 12.17 / 12.13-12.17 / 12.15-12.18 / 12.19-12.22 /
+                           // 12.33 ms per GiB, 64 KiB blocks 13.90 / 13.90-13.92 / 13.93 / 13.95 /
+                           // 14.11, profiles/r06l_*).  Any RMIN >= 1 keeps a window's tokens <= 16
+                           // (62 probe positions, >= 4 bytes per match), so pend <= 48 + 16 = 64
 #endif
 #ifndef SNAPPY_K1R_WINDOW
 #define SNAPPY_K1R_WINDOW 4  // W-probe rounds
@@ -814,7 +817,9 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 // same loop code placed 4 bytes apart measured 1.8 % apart (profiles/r05zn_*,
 // r05zo_*), so the placement is pinned to the measured best instead of being
 // left to the code around the statement.  The padding (s_nop) runs once per
-// entry into the asm loop.
+// entry into the asm loop.  Re-swept with DMAX 13 / 12 and RMIN 2 (profiles/
+// r06n_*): PAD32 0..15 -> 12.18 (2) to 12.79 (13) ms per GiB; PAD64 -1 13.93,
+// 0..14 even 14.00-14.55.
 #ifndef SNAPPY_K1R_PAD32
 #define SNAPPY_K1R_PAD32 2
 #endif

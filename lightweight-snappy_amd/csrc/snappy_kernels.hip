@@ -2309,101 +2309,6 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 const uint32_t last = (uint32_t)__builtin_amdgcn_readlane(pos4, hE - 1) >> 2;
                 hexit = last + (uint32_t)__builtin_amdgcn_readlane(size, last);
             };
-#ifndef SNAPPY_K4_PARSE3
-#define SNAPPY_K4_PARSE3 0
-#endif
-#if SNAPPY_K4_PARSE3
-            if (!(SNAPPY_K4_SPAN_ADAPT && span_cut)) {
-                // three fixed blocks of 64 positions from o, their chains walked
-                // together: the jump tables of all three and block 1's exact exits (X)
-                // by doubling at once; block 0's chain from 0 as its tables grow;
-                // then blocks 1 and 2 from the entries block 0's and block 1's exits
-                // give.  The dependent LDS round trips of a batch drop from about 22
-                // (three halves one after the other) to about 13
-                auto rd = [&](uint32_t x, uint32_t &x0, uint32_t &b4) {
-                    const uint32_t qa = WADR(x);
-                    const uint32_t dA = w32[qa >> 2], dB = w32[(qa >> 2) + 1];
-                    const uint32_t sh = 8 * (qa & 3);
-                    x0 = __builtin_amdgcn_alignbit(dB, dA, sh);
-                    b4 = __builtin_amdgcn_alignbit(dB >> sh, x0, 8);
-                };
-                auto esize = [](uint32_t x0, uint32_t b4) {
-                    const uint32_t tag = x0 & 0xFF, m = tag >> 2, t = tag & 3;
-                    const uint32_t k = __builtin_elementwise_sub_sat(m, 59u);
-                    const uint32_t lv = k ? b4 & (0xFFFFFFFFu >> ((32 - 8 * k) & 31)) : m;
-                    return t == 0 ? lv + k + 2 : (0x5320u >> (4 * t)) & 0xF;
-                };
-                uint32_t s0, s1, s2;
-                {
-                    uint32_t x0, b4;
-                    rd(o + lane, x0, b4);
-                    s0 = esize(x0, b4);
-                    rd(o + 64 + lane, x0, b4);
-                    s1 = esize(x0, b4);
-                    rd(o + 128 + lane, x0, b4);
-                    s2 = esize(x0, b4);
-                }
-#define JUMP(T, a) ({ const uint32_t _a = (a);                                            \
-        const uint32_t _g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)_a, (int)(T));     \
-        _g > _a ? _g : _a; })
-#define XSTEP(J, X) ({ const uint32_t _j = (J);                                           \
-        const uint32_t _g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)_j, (int)(X));     \
-        _j < 256 ? _g : (X); })
-                const uint32_t A1 = 4 * lane + 4 * (s0 < 64 ? s0 : 64);
-                const uint32_t B1 = 4 * lane + 4 * (s1 < 64 ? s1 : 64);
-                const uint32_t C1 = 4 * lane + 4 * (s2 < 64 ? s2 : 64);
-                uint32_t X = lane + s1;  // block 1: the position after the chain from lane leaves it
-                uint32_t p0 = 0;
-                { const uint32_t g = JUMP(A1, p0); p0 = (lane & 1) ? g : p0; }
-                X = XSTEP(B1, X);
-                const uint32_t A2 = JUMP(A1, A1), B2 = JUMP(B1, B1), C2 = JUMP(C1, C1);
-                { const uint32_t g = JUMP(A2, p0); p0 = (lane & 2) ? g : p0; }
-                X = XSTEP(B2, X);
-                const uint32_t A4 = JUMP(A2, A2), B4 = JUMP(B2, B2), C4 = JUMP(C2, C2);
-                { const uint32_t g = JUMP(A4, p0); p0 = (lane & 4) ? g : p0; }
-                X = XSTEP(B4, X);
-                const uint32_t A8 = JUMP(A4, A4), B8 = JUMP(B4, B4), C8 = JUMP(C4, C4);
-                { const uint32_t g = JUMP(A8, p0); p0 = (lane & 8) ? g : p0; }
-                X = XSTEP(B8, X);
-                const uint32_t A16 = JUMP(A8, A8), B16 = JUMP(B8, B8), C16 = JUMP(C8, C8);
-                { const uint32_t g = JUMP(A16, p0); p0 = (lane & 16) ? g : p0; }
-                X = XSTEP(B16, X);
-                // entries: block 0's last element + its size, then block 1's exit
-                // from there (an entry >= 64 skips the block: a long element)
-                const uint32_t E0 = (uint32_t)__builtin_popcountll(__ballot(p0 < 256) & 0xFFFFFFFFull);  // >= 1
-                const uint32_t last0 = (uint32_t)__builtin_amdgcn_readlane(p0, E0 - 1) >> 2;
-                const uint32_t e1 = last0 + (uint32_t)__builtin_amdgcn_readlane(s0, last0) - 64;
-                const uint32_t x1 = e1 < 64 ? (uint32_t)__builtin_amdgcn_readlane(X, e1) : e1;
-                const uint32_t e2 = x1 - 64;
-                uint32_t p1 = 4 * (e1 < 64 ? e1 : 64), p2 = 4 * (e2 < 64 ? e2 : 64);
-                { const uint32_t g = JUMP(B1, p1), h = JUMP(C1, p2); p1 = (lane & 1) ? g : p1; p2 = (lane & 1) ? h : p2; }
-                { const uint32_t g = JUMP(B2, p1), h = JUMP(C2, p2); p1 = (lane & 2) ? g : p1; p2 = (lane & 2) ? h : p2; }
-                { const uint32_t g = JUMP(B4, p1), h = JUMP(C4, p2); p1 = (lane & 4) ? g : p1; p2 = (lane & 4) ? h : p2; }
-                { const uint32_t g = JUMP(B8, p1), h = JUMP(C8, p2); p1 = (lane & 8) ? g : p1; p2 = (lane & 8) ? h : p2; }
-                { const uint32_t g = JUMP(B16, p1), h = JUMP(C16, p2); p1 = (lane & 16) ? g : p1; p2 = (lane & 16) ? h : p2; }
-#undef XSTEP
-#undef JUMP
-                const uint32_t E1 = (uint32_t)__builtin_popcountll(__ballot(p1 < 256) & 0xFFFFFFFFull);
-                const uint32_t E2 = (uint32_t)__builtin_popcountll(__ballot(p2 < 256) & 0xFFFFFFFFull);
-                // lane k <- element k: its window position (every p <= 508, so a
-                // garbage lane's read stays inside the window slots), then its bytes
-                const uint32_t q1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * (lane - E0)), (int)p1);
-                const uint32_t q2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * (lane - E0 - E1)), (int)p2);
-                const uint32_t pk = lane < E0 ? p0 : (lane < E0 + E1 ? q1 + 256 : q2 + 512);
-                rd(o + (pk >> 2), ex0, eb4);
-                E = E0 + E1 + E2 < 64 ? E0 + E1 + E2 : 64;
-#ifdef SNAPPY_K4_STATS
-                n_half += 3;
-#endif
-            } else {
-                uint32_t xa;
-                parse_half(o, ex0, eb4, E, xa);
-#ifdef SNAPPY_K4_STATS
-                n_half++;
-                n_spanb++;
-#endif
-            }
-#else
             uint32_t ax0, ab4, ea, xa;
             parse_half(o, ax0, ab4, ea, xa);
             ex0 = ax0;
@@ -2446,7 +2351,6 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 E = E + eb < 64 ? E + eb : 64;
                 hpos += xb;
             }
-#endif
         }
         // lane k < E holds element k of the batch; lanes >= E hold garbage,
         // masked by `live` / nexec below.  Decode: tag dispatch as selects of

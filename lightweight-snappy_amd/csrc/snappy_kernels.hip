@@ -653,17 +653,14 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             hv = (_pr >> shift) | (__builtin_amdgcn_ubfe(_pr, shift - 8, 8) << 16);                \
         }                                                                                          \
     } while (0)
-// SNAPPY_K1R_WIN_ENT: a window refresh reads the new window's table entries as
-// soon as the addresses are known (their LDS round trip overlaps the lane data)
-// instead of after it
-#ifndef SNAPPY_K1R_WIN_ENT
-#define SNAPPY_K1R_WIN_ENT 1
-#endif
+// A window refresh reads the new window's table entries as soon as the
+// addresses are known (their LDS round trip overlaps the lane data), not after
+// it (the later read: +2.9-3.2 % at every loop placement, profiles/r06q_*)
 #define WINDOW_LS(qq)                                                                              \
     do {                                                                                           \
         WINDOW_AT(qq);                                                                             \
         adr = TBL_ADR(hv & 0xFFFF);                                                                \
-        if (SNAPPY_K1R_WIN_ENT) TBL_READ_ENT(adr); /* in flight during the lane data below */     \
+        TBL_READ_ENT(adr); /* in flight during the lane data below */                             \
         const uint32_t _bits = same_x_bits<DMAX>((hv & 0xFFFF) + 1);                               \
         const uint32_t _pd = _bits ? (uint32_t)__builtin_ctz(_bits) : 0u;                          \
         /* lane - pd + 1, or lane - 1 at pd = 1: pdl1 >= lane0 also implies lane > lane0 */      \
@@ -1063,7 +1060,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             if (!lsw || lane0 + SNAPPY_K1R_RMIN > 62) {
                 refresh();
                 lane0 = 1;
-                went = SNAPPY_K1R_WIN_ENT;
+                went = true;
             }
             // the round's table entries: read right after the round's inserts, so the
             // read is in flight during the verification (each path that writes the table
@@ -1099,7 +1096,6 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                     if (code == 2) {       // the window needs to move
                         refresh();
                         lane0 = 1;
-                        if (!SNAPPY_K1R_WIN_ENT) TBL_READ_ENT(adr);
                         continue;
                     }
                     if (code >= 4) {  // the round stopped after its inserts: finish it here
@@ -1128,7 +1124,6 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                         if (lane0 + SNAPPY_K1R_RMIN > 62) {
                             refresh();
                             lane0 = 1;
-                            if (!SNAPPY_K1R_WIN_ENT) TBL_READ_ENT(adr);
                         }
                         continue;
                     }
@@ -1240,7 +1235,6 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
                 if (__builtin_expect(lane0 + SNAPPY_K1R_RMIN > 62, 0)) {
                     refresh();
                     lane0 = 1;
-                    if (!SNAPPY_K1R_WIN_ENT) TBL_READ_ENT(adr);
                 }
             }
             drain_token();

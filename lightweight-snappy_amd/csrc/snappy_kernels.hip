@@ -2225,6 +2225,11 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
 #ifndef SNAPPY_K4_SPAN_ADAPT
 #define SNAPPY_K4_SPAN_ADAPT 1
 #endif
+// SNAPPY_K4_JSIZE: the batch parse's jumps take a long literal (m >= 60) as
+// leaving the 64 positions; only the last element's exact size is computed
+#ifndef SNAPPY_K4_JSIZE
+#define SNAPPY_K4_JSIZE 0
+#endif
     // the last batch was cut by the 1,024-byte output span (long copies): parse one
     // half only -- more elements would be cut again (repeat-like data)
     bool span_cut = false;
@@ -2270,9 +2275,21 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 // element size: literal 1 + k + (length - 1) + 1, copies 2 / 3 / 5
                 // (src/snappy_decompression.c:290-333)
                 const uint32_t tag = x0 & 0xFF, m = tag >> 2, t = tag & 3;
+#if SNAPPY_K4_JSIZE == 2
+                const uint32_t k = __builtin_elementwise_sub_sat(m, 59u);
+                const uint32_t lv = k ? b4 & (0xFFFFFFFFu >> ((32 - 8 * k) & 31)) : m;
+                const uint32_t xsize = t == 0 ? lv + k + 2 : (0x5320u >> (4 * t)) & 0xF;
+                const uint32_t size = t == 0 ? (m < 60 ? m + 2 : 64u) : (0x5320u >> (4 * t)) & 0xF;
+#elif SNAPPY_K4_JSIZE
+                // for the jumps only: a literal with m >= 60 is >= 63 bytes, taken as
+                // leaving the 64 (at lane 0 it may end at 63: the half then ends one
+                // element early, and the next starts at its exact end, hexit below)
+                const uint32_t size = t == 0 ? (m < 60 ? m + 2 : 64u) : (0x5320u >> (4 * t)) & 0xF;
+#else
                 const uint32_t k = __builtin_elementwise_sub_sat(m, 59u);
                 const uint32_t lv = k ? b4 & (0xFFFFFFFFu >> ((32 - 8 * k) & 31)) : m;
                 const uint32_t size = t == 0 ? lv + k + 2 : (0x5320u >> (4 * t)) & 0xF;
+#endif
                 // positions as ds_bpermute addresses (4 x position); one >= 256 has
                 // left the 64 and must stay >= 256 (its exact value is never used).
                 // Every jump goes forward (an element is >= 2 bytes: T[a / 4] > a for
@@ -2301,7 +2318,22 @@ __device__ __forceinline__ void k4_body(const uint8_t *__restrict__ comp, const 
                 hx0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)pos4, (int)x0);
                 hb4 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)pos4, (int)b4);
                 const uint32_t last = (uint32_t)__builtin_amdgcn_readlane(pos4, hE - 1) >> 2;
+#if SNAPPY_K4_JSIZE == 2
+                hexit = last + (uint32_t)__builtin_amdgcn_readlane(xsize, last);
+#elif SNAPPY_K4_JSIZE
+                {  // the last element's exact size, in scalar registers
+                    const uint32_t lx = (uint32_t)__builtin_amdgcn_readlane(x0, last);
+                    const uint32_t lb = (uint32_t)__builtin_amdgcn_readlane(b4, last);
+                    const uint32_t ltag = lx & 0xFF, lm = ltag >> 2, lt = ltag & 3;
+                    uint32_t lk;  // max(m, 59) - 59 in scalar code (the compiler's saturating form is VALU)
+                    asm("s_max_u32 %0, %1, 59" : "=s"(lk) : "s"(lm) : "scc");
+                    lk -= 59;
+                    const uint32_t llv = lk ? lb & (0xFFFFFFFFu >> ((32 - 8 * lk) & 31)) : lm;
+                    hexit = last + (lt == 0 ? llv + lk + 2 : (0x5320u >> (4 * lt)) & 0xF);
+                }
+#else
                 hexit = last + (uint32_t)__builtin_amdgcn_readlane(size, last);
+#endif
             };
             uint32_t ax0, ab4, ea, xa;
             parse_half(o, ax0, ab4, ea, xa);

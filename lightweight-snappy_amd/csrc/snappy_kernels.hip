@@ -121,13 +121,37 @@ typedef uint16_t __attribute__((aligned(1))) u16u;
 constexpr uint32_t kRegs = 128;  // VGPRs holding a 32 KiB unit (64 dwords each), + 1 zero spare
 // Register r (wave-uniform) of the resident unit.  g0..g3 are pinned to
 // v2..v129 by the asm constraints, so the relative move (s_set_gpr_idx_on,
-// SRC0) is exact whatever else the allocator does.
+// SRC0) is exact whatever else the allocator does.  s_set_gpr_idx_on writes
+// m0, a register the compiler reserves (writelane lane selects) and does not
+// take as an asm clobber.  The statements leave m0 holding the index: the
+// built code object is checked to set m0 again before any later read of it
+// (tools/check_asm_waits.py check_m0, run by tests/test_abi.py).
+// SNAPPY_REGIDX_M0_SAVE 1 saves and restores m0 inside each statement instead
+// (A/B, outputs identical: K1r +1.1 %, K1r64 +0.5 %, profiles/r06w_*).
+#ifndef SNAPPY_REGIDX_M0_SAVE
+#define SNAPPY_REGIDX_M0_SAVE 0
+#endif
+#if SNAPPY_REGIDX_M0_SAVE
+#define REGIDX_M0_DECL uint32_t _m0;
+#define REGIDX_M0_SAVE "s_mov_b32 %[m0s], m0\n\t"
+#define REGIDX_M0_REST "\n\ts_mov_b32 m0, %[m0s]"
+#define REGIDX_M0_OUT , [m0s] "=&s"(_m0)
+#define REGIDX_M0_ONLY [m0s] "=&s"(_m0)
+#else
+#define REGIDX_M0_DECL
+#define REGIDX_M0_SAVE ""
+#define REGIDX_M0_REST ""
+#define REGIDX_M0_OUT
+#define REGIDX_M0_ONLY
+#endif
 #define REG_OF_V(r)                                                                                 \
     ({                                                                                              \
         uint32_t _v;                                                                                \
-        asm volatile("s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\tv_mov_b32 %0, v2\n\ts_set_gpr_idx_off"      \
-                     : "=&v"(_v)                                                                    \
-                     : "s"((uint32_t)(r)), "{v[2:33]}"(g0), "{v[34:65]}"(g1), "{v[66:97]}"(g2),          \
+        REGIDX_M0_DECL                                                                              \
+        asm volatile(REGIDX_M0_SAVE "s_set_gpr_idx_on %[ri], gpr_idx(SRC0)\n\tv_mov_b32 %[ov], v2\n\t"     \
+                     "s_set_gpr_idx_off" REGIDX_M0_REST                                            \
+                     : [ov] "=&v"(_v) REGIDX_M0_OUT                                                  \
+                     : [ri] "s"((uint32_t)(r)), "{v[2:33]}"(g0), "{v[34:65]}"(g1), "{v[66:97]}"(g2),      \
                        "{v[98:129]}"(g3));                                                          \
         _v;                                                                                         \
     })
@@ -140,9 +164,14 @@ constexpr uint32_t kRegs = 128;  // VGPRs holding a 32 KiB unit (64 dwords each)
 // registers (hundreds of spills).  The kernels are checked to keep g0..g3 in
 // place with no VGPR spills (tests/test_abi.py::test_kernel_register_budget).
 #define REG_SET_V(r, val)                                                                            \
-    asm volatile("s_set_gpr_idx_on %0, gpr_idx(DST)\n\tv_mov_b32 v2, %1\n\ts_set_gpr_idx_off"            \
-                 :: "s"((uint32_t)(r)), "v"(val), "{v[2:33]}"(g0), "{v[34:65]}"(g1), "{v[66:97]}"(g2),      \
-                 "{v[98:129]}"(g3) : "memory")
+    do {                                                                                             \
+        REGIDX_M0_DECL                                                                               \
+        asm volatile(REGIDX_M0_SAVE "s_set_gpr_idx_on %[ri], gpr_idx(DST)\n\tv_mov_b32 v2, %[xv]\n\t"       \
+                     "s_set_gpr_idx_off" REGIDX_M0_REST                                             \
+                     : REGIDX_M0_ONLY                                                                \
+                     : [ri] "s"((uint32_t)(r)), [xv] "v"(val), "{v[2:33]}"(g0), "{v[34:65]}"(g1),        \
+                       "{v[66:97]}"(g2), "{v[98:129]}"(g3) : "memory");                              \
+    } while (0)
 #define REG_OF(r)                                                                                   \
     ({                                                                                              \
         const uint32_t _rr = (r);                                                                   \
@@ -156,11 +185,14 @@ constexpr uint32_t kRegs = 128;  // VGPRs holding a 32 KiB unit (64 dwords each)
 // (SRC0 of both moves is indexed); r + 1 = 128 of a 32 KiB unit reads v130,
 // which holds no unit data (see DW_LANES)
 #define REG_PAIR_V(r, lo, hi)                                                                        \
-    asm volatile("s_set_gpr_idx_on %2, gpr_idx(SRC0)\n\tv_mov_b32 %0, v2\n\tv_mov_b32 %1, v3\n\t"           \
-                 "s_set_gpr_idx_off"                                                                 \
-                 : "=&v"(lo), "=&v"(hi)                                                              \
-                 : "s"((uint32_t)(r)), "{v[2:33]}"(g0), "{v[34:65]}"(g1), "{v[66:97]}"(g2),              \
-                   "{v[98:129]}"(g3))
+    do {                                                                                             \
+        REGIDX_M0_DECL                                                                               \
+        asm volatile(REGIDX_M0_SAVE "s_set_gpr_idx_on %[ri], gpr_idx(SRC0)\n\tv_mov_b32 %[olo], v2\n\t"      \
+                     "v_mov_b32 %[ohi], v3\n\ts_set_gpr_idx_off" REGIDX_M0_REST                        \
+                     : [olo] "=&v"(lo), [ohi] "=&v"(hi) REGIDX_M0_OUT                                  \
+                     : [ri] "s"((uint32_t)(r)), "{v[2:33]}"(g0), "{v[34:65]}"(g1), "{v[66:97]}"(g2),      \
+                       "{v[98:129]}"(g3));                                                           \
+    } while (0)
 #define REG_PAIR(r, lo, hi)                                                                          \
     do {                                                                                             \
         const uint32_t _pr = (r);                                                                    \

@@ -208,10 +208,13 @@ def test_asm_memory_ops_drained(tmp_path, obj):
     assert check_asm_waits.check(dis) == []
     if obj.endswith("_d.o"):  # K4's element-start bitmap: clear, or, read in that order
         assert check_asm_waits.check_k4_bitmap(dis) == []
+    else:  # the register-index asm leaves m0 holding its index: nothing reads it after
+        assert check_asm_waits.check_m0(dis) == []
     csrc = os.path.join(ROOT, "lightweight-snappy_amd", "csrc")
     for f in sorted(os.listdir(csrc)):
         if f.endswith(".hip"):
             assert check_asm_waits.lint_source(os.path.join(csrc, f)) == [], f
+            assert check_asm_waits.lint_scc(os.path.join(csrc, f)) == [], f
 
 
 def test_asm_wait_checker_catches_undrained_dma():
@@ -228,3 +231,29 @@ def test_asm_wait_checker_catches_undrained_dma():
          "\ts_endpgm                              // 000000001014: 0\n")
     assert len(check_asm_waits.check(k)) == 1
     assert check_asm_waits.check(k.replace("s_cbranch_scc1 2", "s_nop 1")) == []
+
+
+def test_m0_and_scc_checkers_catch_their_cases(tmp_path):
+    """The checkers themselves: a writelane that reads m0 right after a
+    register-index region is flagged, one after m0 is set again is not; an asm
+    statement with an SCC-writing SALU and no "scc" clobber is flagged."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import check_asm_waits
+    k = ("0000000000001000 <k1r_match_units_x>:\n"
+         "\ts_mov_b32 m0, s4                      // 000000001000: 0\n"
+         "\ts_set_gpr_idx_on s2, gpr_idx(SRC0)    // 000000001004: 0\n"
+         "\tv_mov_b32 v1, v2                      // 00000000100C: 0\n"
+         "\ts_set_gpr_idx_off                     // 000000001010: 0\n"
+         "\tv_writelane_b32 v3, s5, m0            // 000000001014: 0\n"
+         "\ts_endpgm                              // 00000000101C: 0\n")
+    assert len(check_asm_waits.check_m0(k)) == 1
+    fixed = k.replace("\tv_writelane_b32 v3, s5, m0            // 000000001014: 0\n",
+                      "\ts_mov_b32 m0, s4                      // 000000001014: 0\n"
+                      "\tv_writelane_b32 v3, s5, m0            // 000000001018: 0\n")
+    assert check_asm_waits.check_m0(fixed) == []
+    src = tmp_path / "k.hip"
+    src.write_text('asm("s_max_u32 %0, %1, 59" : "=s"(a) : "s"(b));\n'
+                   'asm("s_max_u32 %0, %1, 59" : "=s"(a) : "s"(b) : "scc");\n'
+                   'asm volatile("s_mov_b32 %0, m0\\nL%=_x:" : "=s"(a));\n')
+    assert [b[0].rsplit(":", 1)[1] for b in check_asm_waits.lint_scc(str(src))] == ["1"]

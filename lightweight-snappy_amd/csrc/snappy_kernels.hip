@@ -848,9 +848,10 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 // left to the code around the statement.  The padding (s_nop) runs once per
 // entry into the asm loop.  Re-swept with DMAX 13 / 12 and RMIN 2 (profiles/
 // r06n_*): PAD32 0..15 -> 12.18 (2) to 12.79 (13) ms per GiB; PAD64 -1 13.93,
-// 0..14 even 14.00-14.55.
+// 0..14 even 14.00-14.55.  With SNAPPY_K1R_X45 (r06x_*): PAD32 0 best (12.13-12.20;
+// 12.20-12.53 elsewhere), PAD64 -1 best (13.85-13.88; 13.92-14.53 pinned).
 #ifndef SNAPPY_K1R_PAD32
-#define SNAPPY_K1R_PAD32 2
+#define SNAPPY_K1R_PAD32 0  // with SNAPPY_K1R_X45 (profiles/r06x_*, r06y_*)
 #endif
 #ifndef SNAPPY_K1R_PAD64
 #define SNAPPY_K1R_PAD64 -1
@@ -891,6 +892,32 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     "s_mov_b64 exec, %[sx]\n\t"                                                                     \
     "ds_read_u16 %[ent], %[adr]\n\t" /* the next round's entries */                                  \
     "ds_read_u8 %[entt], %[adrt] offset:%[tagb]\n\t"
+// the match length: lane s1 (the first differing dword of the 64 bytes, -1 if
+// none in lanes 0-31) gives 4 s1 + the byte.  SNAPPY_K1R_X45: one unsigned test
+// of len - 4 > 59 leaves for both rare ends (>= 64 equal bytes: s1 > 15, or -1,
+// whose lane 63 reads >= 252; a tag collision: len < 4), told apart at the exit:
+// one compare and one branch fewer per hit round, K1r 12.18-12.24 -> 12.11-12.17 ms
+// per GiB and K1r64 13.94-13.98 -> 13.82-13.86, each at its best loop placement
+// (profiles/r06x_*, r06y_*, outputs identical)
+#ifndef SNAPPY_K1R_X45
+#define SNAPPY_K1R_X45 1
+#endif
+#if SNAPPY_K1R_X45
+#define K1R_LENCHECK                                                                                \
+    "v_readlane_b32 %[s0], %[t2], %[s1]\n\t"                                                       \
+    "s_add_u32 %[s2], %[s0], -4\n\t"                                                                \
+    "s_cmp_gt_u32 %[s2], 59\n\t"                                                                    \
+    "s_cbranch_scc1 L%=_x4\n\t"
+#define K1R_X4 "s_cmp_lt_u32 %[s0], 4\n\ts_cbranch_scc1 L%=_x5\n\ts_mov_b32 %[code], 4\n\ts_branch L%=_end\n"
+#else
+#define K1R_LENCHECK                                                                                \
+    "s_cmp_gt_u32 %[s1], 15\n\t"                                                                    \
+    "s_cbranch_scc1 L%=_x4\n\t"                                                                    \
+    "v_readlane_b32 %[s0], %[t2], %[s1]\n\t"                                                       \
+    "s_cmp_lt_u32 %[s0], 4\n\t" /* (pf <= L - 16: the clamp below never makes it < 4) */           \
+    "s_cbranch_scc1 L%=_x5\n\t"
+#define K1R_X4 "s_mov_b32 %[code], 4\n\ts_branch L%=_end\n"
+#endif
 #define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, CAND, SEGHI, HIT, PAD)                         \
     do {                                                                                            \
         uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4;                            \
@@ -942,11 +969,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "v_bfe_u32 %[t2], %[t2], 3, 2\n\t"                                                      \
             "v_lshl_or_b32 %[t2], %[lane], 2, %[t2]\n\t" /* the prefix length if this dword differs */ \
             "s_ff1_i32_b32 %[s1], vcc_lo\n\t"                                                       \
-            "s_cmp_gt_u32 %[s1], 15\n\t"                                                            \
-            "s_cbranch_scc1 L%=_x4\n\t"                                                             \
-            "v_readlane_b32 %[s0], %[t2], %[s1]\n\t"                                                \
-            "s_cmp_lt_u32 %[s0], 4\n\t" /* (pf <= L - 16: the clamp below never makes it < 4) */    \
-            "s_cbranch_scc1 L%=_x5\n\t"                                                             \
+            K1R_LENCHECK                                                                            \
             "s_add_u32 %[lane0], %[f], %[s0]\n\t"                                                   \
             "s_pack_ll_b32_b16 %[dka], %[pf], %[s0]\n\t"                                            \
             "s_sub_u32 %[dkb], %[pf], %[c]\n\t"                                                     \
@@ -989,7 +1012,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "L%=_x3:\n\ts_mov_b32 %[code], 3\n\ts_branch L%=_end\n"                                 \
             "L%=_x1:\n\ts_mov_b32 %[code], 1\n\ts_branch L%=_end\n"                                 \
             "L%=_x2:\n\ts_mov_b32 %[code], 2\n\ts_branch L%=_end\n"                                 \
-            "L%=_x4:\n\ts_mov_b32 %[code], 4\n\ts_branch L%=_end\n"                                 \
+            "L%=_x4:\n\t" K1R_X4                                                                   \
             "L%=_far:\n\t" /* K1r64: the candidate's 256 bytes from the input */                    \
             "s_and_b32 %[s1], %[c], -4\n\t"                                                         \
             "v_add_u32_e32 %[t1], %[s1], %[lane4]\n\t"                                              \

@@ -918,6 +918,26 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     "s_cbranch_scc1 L%=_x5\n\t"
 #define K1R_X4 "s_mov_b32 %[code], 4\n\ts_branch L%=_end\n"
 #endif
+// SNAPPY_K1R_EARLY_INS: a hit round's inserts and next entry reads issued as
+// soon as the insert range is known, before the wait for the gathers, which
+// then waits for pa and ca alone (lgkmcnt(4): one wave's LDS operations
+// complete in order; the K1r64 far path's ca is a global load, so there the
+// count leaves pa's four successors); 0: after the funnels (round 5's V18).
+// Measured slower at every loop placement (A/B, outputs identical, 68 GPU tests
+// green on it, profiles/r06z_*: K1r 12.09-12.12 -> 12.18 at best, 12.26-12.59
+// elsewhere; K1r64 equal), so off
+#ifndef SNAPPY_K1R_EARLY_INS
+#define SNAPPY_K1R_EARLY_INS 0
+#endif
+#if SNAPPY_K1R_EARLY_INS
+#define K1R_INS_EARLY K1R_INSERTS("%[s2]", "%[s0]")
+#define K1R_INS_LATE
+#define K1R_GATHER_WAIT "s_waitcnt lgkmcnt(4)\n\t" /* pa and ca; the inserts and entry reads stay in flight */
+#else
+#define K1R_INS_EARLY
+#define K1R_INS_LATE K1R_INSERTS("%[s2]", "%[s0]")
+#define K1R_GATHER_WAIT "s_waitcnt lgkmcnt(0)\n\t" /* pa and ca */
+#endif
 #define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, CAND, SEGHI, HIT, PAD)                         \
     do {                                                                                            \
         uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4;                            \
@@ -954,15 +974,16 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "v_mul_i32_i24_e64 %[t0], %[pf], -8\n\t" /* pa's funnel shift */                        \
             "s_sub_u32 %[s2], %[f], %[s0]\n\t"                                                      \
             "s_add_u32 %[s2], %[s2], 1\n\t" /* lanes lo0 .. f insert */                             \
+            K1R_INS_EARLY                                                                           \
             "s_and_b32 %[s3], %[c], 3\n\t"                                                          \
             "s_mul_i32 %[s3], %[s3], 0xfefefeff\n\t"                                                \
             "s_add_i32 %[s3], %[s3], 0x7060504\n\t" /* ca's perm selector */                        \
-            "s_waitcnt lgkmcnt(0)\n\t" /* pa and ca */                                              \
+            K1R_GATHER_WAIT                                                                         \
             "v_mov_b32_dpp %[t1], %[t2] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
             "v_mov_b32_dpp %[t4], %[t3] wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
             "v_alignbit_b32 %[t2], %[t2], %[t1], %[t0]\n\t"                                         \
             "v_perm_b32 %[t3], %[t3], %[t4], %[s3]\n\t"                                             \
-            K1R_INSERTS("%[s2]", "%[s0]")                                                           \
+            K1R_INS_LATE                                                                            \
             "v_cmp_ne_u32_e32 vcc, %[t2], %[t3]\n\t"                                                \
             "v_xor_b32_e32 %[t2], %[t2], %[t3]\n\t"                                                 \
             "v_ffbh_u32_e32 %[t2], %[t2]\n\t"                                                       \

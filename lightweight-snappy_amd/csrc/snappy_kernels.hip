@@ -944,6 +944,42 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #define K1R_INS_LATE K1R_INSERTS("%[s2]", "%[s0]")
 #define K1R_GATHER_WAIT "s_waitcnt lgkmcnt(0)\n\t" /* pa and ca */
 #endif
+// the miss round's way on: SNAPPY_K1R_NOHIT2 tests the common case first --
+// lane0 <= lim0 = min(62 - RMIN, L - 16 - q0) (window and block end in one
+// signed compare, as the hit path) and skip <= skipmax -- and tells the rare
+// ends apart after it; 0: the four tests in turn.  Two compares and two branches
+// fewer per miss round, yet slower at every loop placement (A/B, outputs
+// identical, profiles/r06ae_*: K1r 12.10-12.13 -> 12.16-12.45 ms per GiB, K1r64
+// 13.57 -> 13.58-13.69), so off
+#ifndef SNAPPY_K1R_NOHIT2
+#define SNAPPY_K1R_NOHIT2 0
+#endif
+#if SNAPPY_K1R_NOHIT2
+#define K1R_NOHIT_TAIL(T)                                                                           \
+    "s_cmp_le_i32 %[lane0], %[lim0]\n\t"                                                           \
+    "s_cbranch_scc0 L%=_nx" T "\n\t"                                                              \
+    "s_cmp_le_u32 %[skip], %[skipmax]\n\t"                                                         \
+    "s_cbranch_scc1 L%=_top" T "\n\t"                                                             \
+    "s_cmp_gt_u32 %[skip], %[lsmax]\n\t"                                                           \
+    "s_cbranch_scc1 L%=_x1\n\t"                                                                    \
+    "s_branch L%=_x3\n"                                                                            \
+    "L%=_nx" T ":\n\t"                                                                            \
+    "s_cmp_gt_u32 %[skip], %[lsmax]\n\t"                                                           \
+    "s_cbranch_scc1 L%=_x1\n\t"                                                                    \
+    "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                               \
+    "s_cbranch_scc1 L%=_x1\n\t"                                                                    \
+    "s_branch L%=_x2\n"
+#else
+#define K1R_NOHIT_TAIL(T)                                                                           \
+    "s_cmp_gt_u32 %[skip], %[lsmax]\n\t"                                                           \
+    "s_cbranch_scc1 L%=_x1\n\t"                                                                    \
+    "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                               \
+    "s_cbranch_scc1 L%=_x1\n\t"                                                                    \
+    "s_cmp_gt_u32 %[lane0], %[l0max]\n\t"                                                          \
+    "s_cbranch_scc1 L%=_x2\n\t"                                                                    \
+    "s_cmp_le_u32 %[skip], %[skipmax]\n\t"                                                         \
+    "s_cbranch_scc1 L%=_top" T "\n"
+#endif
 // one round loop of the asm statement (labels suffixed with T)
 #define K1R_ROUND_BODY(CAND, HIT, T)                                                                \
             "L%=_top" T ":\n\t"                                                                          \
@@ -1021,14 +1057,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "s_add_u32 %[lane0], %[lane0], %[s3]\n\t"                                               \
             "s_add_u32 %[p], %[q0], %[lane0]\n\t"                                                   \
             "s_mov_b32 %[skip], %[s2]\n\t"                                                          \
-            "s_cmp_gt_u32 %[skip], %[lsmax]\n\t"                                                    \
-            "s_cbranch_scc1 L%=_x1\n\t"                                                             \
-            "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                        \
-            "s_cbranch_scc1 L%=_x1\n\t"                                                             \
-            "s_cmp_gt_u32 %[lane0], %[l0max]\n\t"                                                   \
-            "s_cbranch_scc1 L%=_x2\n\t"                                                             \
-            "s_cmp_le_u32 %[skip], %[skipmax]\n\t"                                                  \
-            "s_cbranch_scc1 L%=_top" T "\n"
+            K1R_NOHIT_TAIL(T)
 // SNAPPY_K1R64_HALF32: K1r64's asm statement holds a second round loop with the
 // 32 KiB candidate step, entered while no segment past the first 128 is loaded
 // (seghi == 0: registers 0..127 hold segments 0..127, nothing is far or wrapped;

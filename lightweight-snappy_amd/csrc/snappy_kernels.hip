@@ -851,13 +851,13 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 // 0..14 even 14.00-14.55.  With SNAPPY_K1R_X45 (r06x_*): PAD32 0 best (12.13-12.20;
 // 12.20-12.53 elsewhere), PAD64 -1 best (13.85-13.88; 13.92-14.53 pinned).
 #ifndef SNAPPY_K1R_PAD32
-#define SNAPPY_K1R_PAD32 0  // with SNAPPY_K1R_X45 (profiles/r06x_*, r06y_*)
+#define SNAPPY_K1R_PAD32 2  // with SNAPPY_K1R_EARLY_DK (profiles/r06ag_*, r06ah_*)
 #endif
 #ifndef SNAPPY_K1R_PAD64
 #define SNAPPY_K1R_PAD64 0  // with SNAPPY_K1R64_HALF32 (profiles/r06aa_*, r06ad_*)
 #endif
-#ifndef SNAPPY_K1R_PAD64A  // K1r64's first-32-KiB loop (SNAPPY_K1R64_HALF32)
-#define SNAPPY_K1R_PAD64A 0
+#ifndef SNAPPY_K1R_PAD64A  // K1r64's first-32-KiB loop (SNAPPY_K1R64_HALF32; -1 with EARLY_DK, r06ah_*)
+#define SNAPPY_K1R_PAD64A -1
 #endif
 #ifndef SNAPPY_K1R64_HALF32
 #define SNAPPY_K1R64_HALF32 1
@@ -980,6 +980,22 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
     "s_cmp_le_u32 %[skip], %[skipmax]\n\t"                                                         \
     "s_cbranch_scc1 L%=_top" T "\n"
 #endif
+// SNAPPY_K1R_EARLY_DK: a hit round's token offset written right after the drain
+// that consumed the previous one (in the gather wait's shadow) instead of on the
+// tail after the length read-back.  (The pending flag stays on the tail: the
+// code-5 exit's skip fix reads the previous round's.)  A/B, outputs identical,
+// 68 GPU tests green, at each build's best placements (profiles/r06ag_*, r06ah_*):
+// K1r 12.11-12.13 -> 12.04-12.08 ms per GiB, K1r64 13.55-13.60 -> 13.49-13.51
+#ifndef SNAPPY_K1R_EARLY_DK
+#define SNAPPY_K1R_EARLY_DK 1
+#endif
+#if SNAPPY_K1R_EARLY_DK
+#define K1R_DK_EARLY "s_sub_u32 %[dkb], %[pf], %[c]\n\t"
+#define K1R_DK_LATE "s_mov_b32 %[dkn], 1\n\t"
+#else
+#define K1R_DK_EARLY
+#define K1R_DK_LATE "s_sub_u32 %[dkb], %[pf], %[c]\n\ts_mov_b32 %[dkn], 1\n\t"
+#endif
 // one round loop of the asm statement (labels suffixed with T)
 #define K1R_ROUND_BODY(CAND, HIT, T)                                                                \
             "L%=_top" T ":\n\t"                                                                          \
@@ -1004,6 +1020,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "ds_bpermute_b32 %[t3], %[t1], %[t3]\n\t" /* ca: dwords at c */                         \
             "L%=_farret" T ":\n\t"                                                                       \
             K1R_DRAIN /* the previous round's token, during the gathers */                         \
+            K1R_DK_EARLY                                                                            \
             "s_cmp_lt_u32 %[lane0], %[f]\n\t"                                                       \
             "s_subb_u32 %[s0], %[lane0], 0\n\t" /* lo0 */                                           \
             "v_mul_i32_i24_e64 %[t0], %[pf], -8\n\t" /* pa's funnel shift */                        \
@@ -1028,8 +1045,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             K1R_LENCHECK                                                                            \
             "s_add_u32 %[lane0], %[f], %[s0]\n\t"                                                   \
             "s_pack_ll_b32_b16 %[dka], %[pf], %[s0]\n\t"                                            \
-            "s_sub_u32 %[dkb], %[pf], %[c]\n\t"                                                     \
-            "s_mov_b32 %[dkn], 1\n\t"                                                               \
+            K1R_DK_LATE                                                                             \
             "s_cmp_le_i32 %[lane0], %[lim0]\n\t" /* implies pf + len <= L - 16: no clamp */         \
             "s_cbranch_scc1 L%=_top" T "\n\t"                                                            \
             "s_sub_u32 %[s2], %[L], %[pf]\n\t" /* leaving: the length clamped to the block end */ \

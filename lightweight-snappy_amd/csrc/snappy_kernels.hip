@@ -884,6 +884,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #define K1R_HIT32 K1R_HIT_PREDTAG
 #define K1R_HIT64 K1R_HIT_PREDTAG
 #define K1R_DRAIN                                                                                   \
+    K1R_DRAIN_PACK                                                                                  \
     "s_mov_b32 m0, %[pend]\n\t" /* (gfx950 refuses two SGPRs in a v_writelane: m0 stays) */          \
     "v_writelane_b32 %[tka], %[dka], m0\n\t"                                                        \
     "v_writelane_b32 %[tkb], %[dkb], m0\n\t"                                                        \
@@ -908,13 +909,39 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #ifndef SNAPPY_K1R_X45
 #define SNAPPY_K1R_X45 1
 #endif
+// SNAPPY_K1R_PACK_DRAIN: a hit round leaves its token as pf (dka) and the length
+// (dlen, the read-back's own register) and the next round's drain packs them
+// (one s_pack in the drain, one s_mov of pf in the gather wait's shadow) instead
+// of an s_pack on the tail after the length read-back; every exit that keeps a
+// token pending packs it itself (the leaving path) or hands it to C++ (codes 4/5).
+// Slower at every loop placement (A/B, outputs identical, 68 GPU tests green,
+// profiles/r06aj_*: K1r 12.04 -> 12.18 at best, K1r64 13.49-13.51 -> 13.67 at
+// best: the pack now sits on the next round's drain before its writelanes), so off
+#ifndef SNAPPY_K1R_PACK_DRAIN
+#define SNAPPY_K1R_PACK_DRAIN 0
+#endif
+#if SNAPPY_K1R_PACK_DRAIN
+#define K1R_LEN "%[dlen]"
+#define K1R_DRAIN_PACK "s_pack_ll_b32_b16 %[dka], %[dka], %[dlen]\n\t"
+#define K1R_DKA_SHADOW "s_mov_b32 %[dka], %[pf]\n\t"
+#define K1R_DKA_TAIL
+#define K1R_DLEN_DECL uint32_t _dlen = dka >> 16; /* the pending token's length */
+#define K1R_DLEN_OP [dlen] "+s"(_dlen),
+#else
+#define K1R_LEN "%[s0]"
+#define K1R_DRAIN_PACK
+#define K1R_DKA_SHADOW
+#define K1R_DKA_TAIL "s_pack_ll_b32_b16 %[dka], %[pf], %[s0]\n\t"
+#define K1R_DLEN_DECL
+#define K1R_DLEN_OP
+#endif
 #if SNAPPY_K1R_X45
 #define K1R_LENCHECK                                                                                \
-    "v_readlane_b32 %[s0], %[t2], %[s1]\n\t"                                                       \
-    "s_add_u32 %[s2], %[s0], -4\n\t"                                                                \
+    "v_readlane_b32 " K1R_LEN ", %[t2], %[s1]\n\t"                                                 \
+    "s_add_u32 %[s2], " K1R_LEN ", -4\n\t"                                                          \
     "s_cmp_gt_u32 %[s2], 59\n\t"                                                                    \
     "s_cbranch_scc1 L%=_x4\n\t"
-#define K1R_X4 "s_cmp_lt_u32 %[s0], 4\n\ts_cbranch_scc1 L%=_x5\n\ts_mov_b32 %[code], 4\n\ts_branch L%=_end\n"
+#define K1R_X4 "s_cmp_lt_u32 " K1R_LEN ", 4\n\ts_cbranch_scc1 L%=_x5\n\ts_mov_b32 %[code], 4\n\ts_branch L%=_end\n"
 #else
 #define K1R_LENCHECK                                                                                \
     "s_cmp_gt_u32 %[s1], 15\n\t"                                                                    \
@@ -1021,6 +1048,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "L%=_farret" T ":\n\t"                                                                       \
             K1R_DRAIN /* the previous round's token, during the gathers */                         \
             K1R_DK_EARLY                                                                            \
+            K1R_DKA_SHADOW                                                                          \
             "s_cmp_lt_u32 %[lane0], %[f]\n\t"                                                       \
             "s_subb_u32 %[s0], %[lane0], 0\n\t" /* lo0 */                                           \
             "v_mul_i32_i24_e64 %[t0], %[pf], -8\n\t" /* pa's funnel shift */                        \
@@ -1043,16 +1071,16 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "v_lshl_or_b32 %[t2], %[lane], 2, %[t2]\n\t" /* the prefix length if this dword differs */ \
             "s_ff1_i32_b32 %[s1], vcc_lo\n\t"                                                       \
             K1R_LENCHECK                                                                            \
-            "s_add_u32 %[lane0], %[f], %[s0]\n\t"                                                   \
-            "s_pack_ll_b32_b16 %[dka], %[pf], %[s0]\n\t"                                            \
+            "s_add_u32 %[lane0], %[f], " K1R_LEN "\n\t"                                             \
+            K1R_DKA_TAIL                                                                            \
             K1R_DK_LATE                                                                             \
             "s_cmp_le_i32 %[lane0], %[lim0]\n\t" /* implies pf + len <= L - 16: no clamp */         \
             "s_cbranch_scc1 L%=_top" T "\n\t"                                                            \
             "s_sub_u32 %[s2], %[L], %[pf]\n\t" /* leaving: the length clamped to the block end */ \
-            "s_min_u32 %[s0], %[s0], %[s2]\n\t"                                                     \
-            "s_add_u32 %[p], %[pf], %[s0]\n\t"                                                      \
+            "s_min_u32 " K1R_LEN ", " K1R_LEN ", %[s2]\n\t"                                          \
+            "s_add_u32 %[p], %[pf], " K1R_LEN "\n\t"                                                \
             "s_sub_u32 %[lane0], %[p], %[q0]\n\t"                                                   \
-            "s_lshl_b32 %[s1], %[s0], 16\n\t"                                                       \
+            "s_lshl_b32 %[s1], " K1R_LEN ", 16\n\t"                                                 \
             "s_or_b32 %[dka], %[s1], %[pf]\n\t"                                                     \
             "s_cmp_gt_u32 %[p], %[lm16]\n\t"                                                        \
             "s_cbranch_scc1 L%=_x1\n\t"                                                             \
@@ -1094,6 +1122,7 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
 #define K1R_ASM_ROUNDS_STMT(code, fx, cx, e32, et32, CAND, SEGHI, HIT, PAD, DUAL_SEL, DUAL_LOOP)    \
     do {                                                                                            \
         uint32_t _m0s, _pf, _s0, _s1, _s2, _s3, _t0, _t1, _t2, _t3, _t4;                            \
+        K1R_DLEN_DECL                                                                               \
         uint64_t _valid, _hm;                                                                       \
         asm volatile(                                                                               \
             "s_mov_b32 %[m0s], m0\n\t"                                                              \
@@ -1129,7 +1158,8 @@ __device__ __forceinline__ void k1r_body(const uint8_t *__restrict__ in, uint64_
             "s_mov_b32 m0, %[m0s]\n\t"                                                              \
             "s_waitcnt lgkmcnt(0)"                                                                  \
             : [p] "+s"(p), [skip] "+s"(skip), [lane0] "+s"(lane0), [pend] "+s"(pend), [dka] "+s"(dka), \
-              [dkb] "+s"(dkb), [dkn] "+s"(dkn), [code] "=&s"(code), [f] "=&s"(fx), [c] "=&s"(cx),      \
+              [dkb] "+s"(dkb), [dkn] "+s"(dkn), K1R_DLEN_OP [code] "=&s"(code), [f] "=&s"(fx),         \
+              [c] "=&s"(cx),                                                                        \
               [m0s] "=&s"(_m0s), [pf] "=&s"(_pf), [s0] "=&s"(_s0), [s1] "=&s"(_s1), [s2] "=&s"(_s2),   \
               [s3] "=&s"(_s3), [valid] "=&s"(_valid), [hm] "=&s"(_hm), [ent] "+v"(e32),                \
               [entt] "+v"(et32), [tka] "+v"(tka), [tkb] "+v"(tkb), [t0] "=&v"(_t0), [t1] "=&v"(_t1),  \
